@@ -1,0 +1,44 @@
+# Native build of the MI355X path tracer.  `make` (or __graft_entry__.build()) builds in-tree:
+#   pathtracercuda_amd/lib/libpt_hip.so   HIP kernels + device C ABI (include/pt_hip.h), gfx950
+#   pathtracercuda_amd/lib/libpt_host.so  host C++ layer + C ABI (include/pathtracer_amd.hpp, pt_host.h)
+#   pathtracercuda_amd/lib/pathtracer     CLI (reference main.cpp headless path)
+#   oracle/liboracle.so                   CPU restatement (test infrastructure only)
+# Every FP unit is built with -ffp-contract=off: the GPU result is compared bit for bit with the
+# oracle, and the host-built BVH / transforms / camera feed the GPU directly.
+HIPCC ?= /opt/rocm/bin/hipcc
+CXX ?= g++
+ARCH ?= gfx950
+LIB := pathtracercuda_amd/lib
+SRC := pathtracercuda_amd/csrc
+HOST_SRCS := $(SRC)/host/math_camera.cpp $(SRC)/host/hittable.cpp $(SRC)/host/bvh_build.cpp \
+             $(SRC)/host/json_min.cpp $(SRC)/host/scene_json.cpp $(SRC)/host/image_io.cpp \
+             $(SRC)/host/renderer.cpp $(SRC)/host/host_capi.cpp
+HOST_HDRS := include/pathtracer_amd.hpp include/pt_host.h include/pt_hip.h $(SRC)/host/host_internal.h $(SRC)/host/json_min.h
+
+HIPFLAGS ?= --offload-arch=$(ARCH) -O3 -std=c++17 -ffp-contract=off -fPIC -fvisibility=hidden \
+            -mcode-object-version=5 -Iinclude -Wall -Wno-unused-result
+CXXFLAGS ?= -O2 -std=c++17 -ffp-contract=off -fno-fast-math -fPIC -Iinclude -I$(SRC)/host -Wall -Wextra \
+            -Wno-unused-parameter -Wno-missing-field-initializers
+
+all: $(LIB)/libpt_hip.so $(LIB)/libpt_host.so $(LIB)/pathtracer oracle
+
+$(LIB):
+	mkdir -p $(LIB)
+
+$(LIB)/libpt_hip.so: $(SRC)/pt_kernels.hip $(SRC)/pt_math.h include/pt_hip.h | $(LIB)
+	$(HIPCC) $(HIPFLAGS) -shared -o $@ $(SRC)/pt_kernels.hip
+
+$(LIB)/libpt_host.so: $(HOST_SRCS) $(HOST_HDRS) $(LIB)/libpt_hip.so
+	$(CXX) $(CXXFLAGS) -shared -o $@ $(HOST_SRCS) -L$(LIB) -lpt_hip -lz -Wl,-rpath,'$$ORIGIN'
+
+$(LIB)/pathtracer: $(SRC)/host/cli_main.cpp $(LIB)/libpt_host.so
+	$(CXX) $(CXXFLAGS) -o $@ $(SRC)/host/cli_main.cpp -L$(LIB) -lpt_host -lpt_hip -lpthread -Wl,-rpath,'$$ORIGIN'
+
+oracle:
+	$(MAKE) -C oracle
+
+clean:
+	rm -f $(LIB)/libpt_hip.so $(LIB)/libpt_host.so $(LIB)/pathtracer
+	$(MAKE) -C oracle clean
+
+.PHONY: all oracle clean

@@ -1,0 +1,149 @@
+/*
+ * pt_hip.h -- C ABI of the MI355X (gfx950) path-tracing device layer, libpt_hip.so.
+ *
+ * This is the drop-in boundary below the reference's `Pathtracer` class: it replaces the CUDA
+ * resource management and kernel launches of PathtracerCUDA/src/pathtracer/Pathtracer.cpp and the
+ * three kernels of src/pathtracer/kernels/ (trace.cu, initRandState.cu, tonemap.cu).  Plain C:
+ * POD structs, pointers and sizes only; no C++ or torch types.  The host C++ layer
+ * (include/pt_host.h, libpt_host.so) owns scene loading, the SAH BVH build and the frame counter,
+ * exactly as the reference's host code does, and calls down into these entry points.
+ *
+ * Every call returns PT_OK (0) or a PT_ERR_* code; pt_last_error() gives the message.  All calls
+ * on one context must come from one host thread (reference: single thread, Pathtracer.cpp:40).
+ */
+#ifndef PT_HIP_H
+#define PT_HIP_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define PT_API __attribute__((visibility("default")))
+
+enum {
+    PT_OK = 0,
+    PT_ERR_HIP = 1,        /* a HIP runtime call failed (reference: checkCudaErrors -> exit) */
+    PT_ERR_ARG = 2,        /* invalid argument */
+    PT_ERR_STATE = 3,      /* call not valid in the current state */
+    PT_ERR_DEPTH = 4,      /* BVH deeper than the 32-entry traversal stack (trace.cu:39) allows */
+    PT_ERR_NO_DEVICE = 5   /* no GPU visible */
+};
+
+#define PT_MAX_TEXTURES 64 /* Pathtracer.cpp:15 MAX_TEXTURE_COUNT */
+
+/* Camera (reference Camera.h:14-22, 92 B, passed by value to traceKernel, trace.h:20) */
+typedef struct pt_camera {
+    float tan_half_fovy;
+    float aspect_ratio;
+    float origin[3];
+    float lower_left_corner[3];
+    float horizontal[3];
+    float vertical[3];
+    float right[3];
+    float up[3];
+    float backward[3];
+} pt_camera;
+
+/* BVH node (reference BVH.h:6-11, 32 B): interior nodes have primitive count 0 in bits 16-31 and
+ * the split axis in bits 8-15; left child = index + 1, right child = offset; leaves hold the first
+ * primitive index in offset. */
+typedef struct pt_bvh_node {
+    float aabb_min[3];
+    float aabb_max[3];
+    uint32_t offset;
+    uint32_t primitive_count_axis;
+} pt_bvh_node;
+
+/* Device hittable (reference Hittable.h:23-27 + Material.h:22-27, 96 B): world->object 3x4 rows,
+ * material, shape type (0 SPHERE .. 6 CUBE, Hittable.h:9-12); material_type 0 LAMBERT, 1 GGX,
+ * 2 LAMBERT_GGX (Material.h:9-12); texture_index is a 1-based handle, 0 = none. */
+typedef struct pt_hittable {
+    float inv_transform_rows[3][4];
+    float base_color[3];
+    float roughness;
+    float emissive[3];
+    float metalness;
+    uint32_t texture_index;
+    uint32_t material_type;
+    uint32_t type;
+    uint32_t pad;
+} pt_hittable;
+
+/* Traversal statistics of an instrumented render (for the algorithmic-byte count of DESIGN.md). */
+typedef struct pt_render_stats {
+    uint64_t node_tests;   /* AABB::hit calls                         */
+    uint64_t prim_tests;   /* Hittable::hit calls                     */
+    uint64_t hits;         /* segments that hit a primitive           */
+    uint64_t sky_lookups;  /* misses that sampled the skybox texture  */
+    uint64_t segments;     /* hitBVH calls                            */
+    uint64_t samples;      /* camera paths                            */
+} pt_render_stats;
+
+typedef struct pt_context pt_context;
+
+/* Number of visible GPUs. */
+PT_API int pt_device_count(int *count);
+
+/* Pathtracer ctor (Pathtracer.cpp:30-68): allocates the accumulation buffer and the per-pixel
+ * XORWOW state and seeds it with curand_init(1984 + x + y * width, 0, 0) (initRandState.cu:16).
+ * The context covers rows y = row_offset + k * row_stride (k = 0 .. local rows - 1) of a
+ * width x height image, so an image can be tiled across GPUs (row_offset = rank, row_stride = N);
+ * seeds and camera coordinates always use global pixel coordinates. */
+PT_API int pt_create(int device, uint32_t width, uint32_t height, uint32_t row_offset, uint32_t row_stride,
+                     pt_context **out);
+PT_API void pt_destroy(pt_context *ctx);
+
+/* Pathtracer::setScene upload half (Pathtracer.cpp:137-159): nodes and primitives as produced by
+ * the host BVH build (elements already reordered).  Replaces the previous scene.  Returns
+ * PT_ERR_DEPTH if a traversal could overflow the reference's 32-entry stack. */
+PT_API int pt_set_scene(pt_context *ctx, const pt_bvh_node *nodes, uint32_t node_count, const pt_hittable *prims,
+                        uint32_t prim_count);
+
+/* Pathtracer::loadTexture upload half (Pathtracer.cpp:258-288): RGBA float texels (LDR textures
+ * already normalised to [0,1]), row 0 = first image row; handle is 1-based (1..64).  Sampled with
+ * bilinear filtering, wrap in u, clamp in v, normalised coordinates. */
+PT_API int pt_set_texture(pt_context *ctx, uint32_t handle, const float *rgba, uint32_t width, uint32_t height);
+
+/* Pathtracer::setSkyboxTextureHandle (Pathtracer.cpp:294-297); 0 = no skybox (black). */
+PT_API int pt_set_skybox(pt_context *ctx, uint32_t handle);
+
+/* traceKernel launch (Pathtracer.cpp:162-199, trace.cu:158-199).  Equivalent to `chunks`
+ * successive reference render(camera, spp, ignore) calls where the first call uses
+ * ignore = ignore_history and the others ignore = false (the headless loop, main.cpp:275-279).
+ * Synchronous.  gpu_ms (optional) receives the kernel time measured with hipEvents on the
+ * context's stream.  No launch (and no error) when no scene is set or spp == 0, as in the
+ * reference (Pathtracer.cpp:174). */
+PT_API int pt_render(pt_context *ctx, const pt_camera *camera, uint32_t spp, uint32_t chunks, int ignore_history,
+                     float *gpu_ms);
+
+/* Same as pt_render with the instrumented kernel variant: identical results plus counters. */
+PT_API int pt_render_instrumented(pt_context *ctx, const pt_camera *camera, uint32_t spp, uint32_t chunks,
+                           int ignore_history, float *gpu_ms, pt_render_stats *stats);
+
+/* Raw accumulation sums (float4 per local pixel, rows x width, y-up), the data behind
+ * getHDRImageData (Pathtracer.cpp:299-315) before the division by the frame count. */
+PT_API int pt_read_accum(pt_context *ctx, float *dst);
+
+/* Device-to-device copy of the raw accumulation buffer (rows * width * 16 bytes) into memory of
+ * the same device, e.g. a send buffer for the multi-GPU framebuffer gather. */
+PT_API int pt_copy_accum_device(pt_context *ctx, void *dst_device, size_t bytes);
+
+/* tonemap kernel (tonemap.cu:4-27) over the local rows: accum / frames, Reinhard, gamma 2.2,
+ * truncation to 8 bits, alpha 255 (RGBA8, rows x width). */
+PT_API int pt_tonemap(pt_context *ctx, uint32_t frames, uint8_t *dst);
+
+/* Per-pixel XORWOW state (d, v0..v4 as uint32, rows x width x 6) -- for tests/checkpoints. */
+PT_API int pt_read_rng(pt_context *ctx, uint32_t *dst);
+PT_API int pt_write_rng(pt_context *ctx, const uint32_t *src);
+
+PT_API uint32_t pt_local_rows(const pt_context *ctx);
+PT_API const char *pt_last_error(const pt_context *ctx);
+
+#ifdef __cplusplus
+}
+#endif
+
+#endif /* PT_HIP_H */

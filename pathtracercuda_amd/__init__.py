@@ -1,0 +1,218 @@
+"""MI355X-native path tracer with the capabilities of DoerriesT/PathtracerCUDA's hot path.
+
+Python mirror of the reference's host interface (PathtracerCUDA/src/pathtracer/Pathtracer.h:12-68,
+SceneLoader.h, Camera.h) over the native libraries:
+
+    pt = Pathtracer(width, height)            # Pathtracer(w, h)            Pathtracer.cpp:30
+    cam = pt.load_scene("scene.json")         # loadScene(pt, params)        SceneLoader.cpp:124
+    pt.render(cam, 8, ignore_history=True)    # render(camera, spp, ignore)  Pathtracer.cpp:162
+    ms = pt.get_timing()                      # getTiming()                  Pathtracer.cpp:229
+    hdr = pt.get_hdr_image_data()             # getHDRImageData()            Pathtracer.cpp:299
+    rgba8 = pt.get_image_data()               # getImageData()               Pathtracer.cpp:317
+
+All rendering runs in hand-written HIP kernels for gfx950 (libpt_hip.so); scene loading, the SAH
+BVH and frame accounting run in host C++ (libpt_host.so).  There is no CPU fallback.
+"""
+from __future__ import annotations
+
+import ctypes as C
+import os
+from typing import Dict, Optional, Sequence
+
+import numpy as np
+
+from . import _native as N
+from ._native import PathtracerError, PtBvhNode, PtCamera, PtHittable, PtRenderStats, device_count
+
+__all__ = ["Pathtracer", "Scene", "make_camera", "radians", "device_count", "PathtracerError", "PtCamera",
+           "PtBvhNode", "PtHittable", "write_png", "write_hdr", "HITTABLE_TYPES", "MATERIAL_TYPES"]
+
+HITTABLE_TYPES = ["SPHERE", "CYLINDER", "DISK", "CONE", "PARABOLOID", "QUAD", "CUBE"]   # Hittable.h:9-12
+MATERIAL_TYPES = ["LAMBERT", "GGX", "LAMBERT_GGX"]                                     # Material.h:9-12
+
+
+def _f3(v: Sequence[float]):
+    return (C.c_float * 3)(*[float(np.float32(x)) for x in v])
+
+
+def radians(degrees: float) -> float:
+    """SceneLoader.cpp:193-196 (float arithmetic)."""
+    return float(N.host().pth_radians(float(degrees)))
+
+
+def make_camera(position, look_at, up=(0.0, 1.0, 0.0), fovy_radians: float = 1.0471976, aspect: float = 1.0) -> PtCamera:
+    """Camera ctor (Camera.inl:4-23)."""
+    cam = PtCamera()
+    N.check_host(N.host().pth_camera_make(_f3(position), _f3(look_at), _f3(up), float(fovy_radians), float(aspect),
+                                          C.byref(cam)))
+    return cam
+
+
+def write_png(path: str, rgba: np.ndarray, flip: bool = True) -> None:
+    a = np.ascontiguousarray(rgba, dtype=np.uint8)
+    h, w = a.shape[:2]
+    N.check_host(N.host().pth_write_png(os.fsencode(path), w, h, a.ctypes.data_as(C.POINTER(C.c_uint8)), int(flip)))
+
+
+def write_hdr(path: str, rgba: np.ndarray, flip: bool = True) -> None:
+    a = np.ascontiguousarray(rgba, dtype=np.float32)
+    h, w = a.shape[:2]
+    N.check_host(N.host().pth_write_hdr(os.fsencode(path), w, h, a.ctypes.data_as(C.POINTER(C.c_float)), int(flip)))
+
+
+class Scene:
+    """A parsed scene file (no GPU): objects in file order, the SAH BVH, camera, textures."""
+
+    def __init__(self, path: str, width: int, height: int) -> None:
+        self._h = C.c_void_p()
+        N.check_host(N.host().pth_scene_load(os.fsencode(str(path)), int(width), int(height), C.byref(self._h)))
+        self.path = str(path)
+
+    def __del__(self) -> None:
+        h = getattr(self, "_h", None)
+        if h:
+            N.host().pth_scene_free(h)
+            self._h = None
+
+    @property
+    def object_count(self) -> int:
+        return int(N.host().pth_scene_object_count(self._h))
+
+    @property
+    def node_count(self) -> int:
+        return int(N.host().pth_scene_node_count(self._h))
+
+    @property
+    def bvh_depth(self) -> int:
+        return int(N.host().pth_scene_bvh_depth(self._h))
+
+    def objects(self):
+        n = self.object_count
+        objs = (PtHittable * max(1, n))()
+        aabbs = np.zeros((n, 6), dtype=np.float32)
+        N.check_host(N.host().pth_scene_objects(self._h, objs, aabbs.ctypes.data_as(C.POINTER(C.c_float))))
+        return objs, aabbs
+
+    def bvh(self):
+        nodes = (PtBvhNode * max(1, self.node_count))()
+        prims = (PtHittable * max(1, self.object_count))()
+        N.check_host(N.host().pth_scene_bvh(self._h, nodes, prims))
+        return nodes, prims
+
+    def camera(self) -> PtCamera:
+        cam = PtCamera()
+        N.check_host(N.host().pth_scene_camera(self._h, C.byref(cam)))
+        return cam
+
+    @property
+    def skybox(self) -> int:
+        return int(N.host().pth_scene_skybox(self._h))
+
+    def textures(self):
+        out = []
+        for handle in range(1, int(N.host().pth_scene_texture_count(self._h)) + 1):
+            w, h = C.c_uint32(), C.c_uint32()
+            N.check_host(N.host().pth_scene_texture_info(self._h, handle, C.byref(w), C.byref(h)))
+            t = np.zeros((h.value, w.value, 4), dtype=np.float32)
+            N.check_host(N.host().pth_scene_texture_data(self._h, handle, t.ctypes.data_as(C.POINTER(C.c_float))))
+            out.append(t)
+        return out
+
+
+class Pathtracer:
+    """The reference's Pathtracer on one MI355X (or on the row tile y = row_offset + k * row_stride)."""
+
+    def __init__(self, width: int, height: int, device: int = 0, row_offset: int = 0, row_stride: int = 1) -> None:
+        self._r = C.c_void_p()
+        N.check_host(N.host().pth_renderer_create(int(width), int(height), int(device), int(row_offset),
+                                                  int(row_stride), C.byref(self._r)))
+        self.width, self.height = int(width), int(height)
+        self.device = int(device)
+        self.row_offset, self.row_stride = int(row_offset), int(row_stride)
+        self.rows = int(N.host().pth_renderer_local_rows(self._r))
+        self._ctx = N.host().pth_renderer_context(self._r)
+
+    def close(self) -> None:
+        if getattr(self, "_r", None):
+            N.host().pth_renderer_destroy(self._r)
+            self._r = None
+
+    def __del__(self) -> None:
+        self.close()
+
+    def __enter__(self) -> "Pathtracer":
+        return self
+
+    def __exit__(self, *exc) -> None:
+        self.close()
+
+    # --- reference API --------------------------------------------------------------------------
+    def load_scene(self, path: str) -> PtCamera:
+        cam = PtCamera()
+        N.check_host(N.host().pth_renderer_load_scene(self._r, os.fsencode(str(path)), C.byref(cam)))
+        return cam
+
+    def render(self, camera: PtCamera, spp: int, ignore_history: bool, chunks: int = 1) -> None:
+        """`chunks` x render(camera, spp, ignore_history and first) in one kernel launch."""
+        N.check_host(N.host().pth_renderer_render(self._r, C.byref(camera), int(spp), int(chunks), int(bool(ignore_history))))
+
+    def get_timing(self) -> float:
+        return float(N.host().pth_renderer_timing(self._r))
+
+    @property
+    def frames(self) -> int:
+        return int(N.host().pth_renderer_frames(self._r))
+
+    def get_hdr_image_data(self) -> np.ndarray:
+        p = N.host().pth_renderer_hdr(self._r)
+        if not p:
+            N.check_host(N.PT_ERR_HIP)
+        return np.ctypeslib.as_array(p, shape=(self.rows, self.width, 4)).copy()
+
+    def get_image_data(self) -> np.ndarray:
+        p = N.host().pth_renderer_image(self._r)
+        if not p:
+            N.check_host(N.PT_ERR_HIP)
+        return np.ctypeslib.as_array(p, shape=(self.rows, self.width, 4)).copy()
+
+    # --- device-layer access (C ABI of pt_hip.h) ------------------------------------------------
+    def accum(self) -> np.ndarray:
+        """Raw accumulation sums (rows x width x 4 float32)."""
+        out = np.zeros((self.rows, self.width, 4), dtype=np.float32)
+        N.check_ctx(N.hip().pt_read_accum(self._ctx, out.ctypes.data_as(C.POINTER(C.c_float))), self._ctx)
+        return out
+
+    def rng_state(self) -> np.ndarray:
+        out = np.zeros((self.rows, self.width, 6), dtype=np.uint32)
+        N.check_ctx(N.hip().pt_read_rng(self._ctx, out.ctypes.data_as(C.POINTER(C.c_uint32))), self._ctx)
+        return out
+
+    def set_rng_state(self, state: np.ndarray) -> None:
+        s = np.ascontiguousarray(state, dtype=np.uint32)
+        assert s.shape == (self.rows, self.width, 6)
+        N.check_ctx(N.hip().pt_write_rng(self._ctx, s.ctypes.data_as(C.POINTER(C.c_uint32))), self._ctx)
+
+    def render_raw(self, camera: PtCamera, spp: int, chunks: int, ignore_history: bool) -> float:
+        """Device-layer launch without frame accounting; returns the kernel time in ms."""
+        ms = C.c_float(0.0)
+        N.check_ctx(N.hip().pt_render(self._ctx, C.byref(camera), int(spp), int(chunks), int(bool(ignore_history)),
+                                      C.byref(ms)), self._ctx)
+        return float(ms.value)
+
+    def render_instrumented(self, camera: PtCamera, spp: int, chunks: int, ignore_history: bool) -> Dict[str, int]:
+        ms = C.c_float(0.0)
+        st = PtRenderStats()
+        N.check_ctx(N.hip().pt_render_instrumented(self._ctx, C.byref(camera), int(spp), int(chunks),
+                                                   int(bool(ignore_history)), C.byref(ms), C.byref(st)), self._ctx)
+        d = {name: int(getattr(st, name)) for name, _ in PtRenderStats._fields_}
+        d["ms"] = float(ms.value)
+        return d
+
+    def copy_accum_to_device(self, dst_ptr: int, nbytes: int) -> None:
+        N.check_ctx(N.hip().pt_copy_accum_device(self._ctx, C.c_void_p(int(dst_ptr)), int(nbytes)), self._ctx)
+
+    def tonemap(self, frames: Optional[int] = None) -> np.ndarray:
+        out = np.zeros((self.rows, self.width, 4), dtype=np.uint8)
+        f = self.frames if frames is None else int(frames)
+        N.check_ctx(N.hip().pt_tonemap(self._ctx, f, out.ctypes.data_as(C.POINTER(C.c_uint8))), self._ctx)
+        return out

@@ -1,0 +1,147 @@
+"""ctypes bindings of the native libraries (include/pt_hip.h, include/pt_host.h).
+
+The libraries are built in-tree by `make` (or __graft_entry__.build()) into
+pathtracercuda_amd/lib/.  There is no fallback: if they are missing the import fails loudly.
+"""
+from __future__ import annotations
+
+import ctypes as C
+import pathlib
+
+LIB_DIR = pathlib.Path(__file__).resolve().parent / "lib"
+HIP_LIB = LIB_DIR / "libpt_hip.so"
+HOST_LIB = LIB_DIR / "libpt_host.so"
+CLI = LIB_DIR / "pathtracer"
+
+PT_OK, PT_ERR_HIP, PT_ERR_ARG, PT_ERR_STATE, PT_ERR_DEPTH, PT_ERR_NO_DEVICE = range(6)
+PT_MAX_TEXTURES = 64
+
+
+class PtCamera(C.Structure):
+    """pt_camera (reference Camera.h:14-22)."""
+    _fields_ = [("tan_half_fovy", C.c_float), ("aspect_ratio", C.c_float), ("origin", C.c_float * 3),
+                ("lower_left_corner", C.c_float * 3), ("horizontal", C.c_float * 3), ("vertical", C.c_float * 3),
+                ("right", C.c_float * 3), ("up", C.c_float * 3), ("backward", C.c_float * 3)]
+
+
+class PtBvhNode(C.Structure):
+    """pt_bvh_node (reference BVH.h:6-11)."""
+    _fields_ = [("aabb_min", C.c_float * 3), ("aabb_max", C.c_float * 3), ("offset", C.c_uint32),
+                ("primitive_count_axis", C.c_uint32)]
+
+
+class PtHittable(C.Structure):
+    """pt_hittable (reference Hittable.h:23-27 + Material.h:22-27)."""
+    _fields_ = [("inv_transform_rows", (C.c_float * 4) * 3), ("base_color", C.c_float * 3), ("roughness", C.c_float),
+                ("emissive", C.c_float * 3), ("metalness", C.c_float), ("texture_index", C.c_uint32),
+                ("material_type", C.c_uint32), ("type", C.c_uint32), ("pad", C.c_uint32)]
+
+
+class PtRenderStats(C.Structure):
+    _fields_ = [("node_tests", C.c_uint64), ("prim_tests", C.c_uint64), ("hits", C.c_uint64),
+                ("sky_lookups", C.c_uint64), ("segments", C.c_uint64), ("samples", C.c_uint64)]
+
+
+# symbol -> (restype, argtypes); the CPU test suite checks that every declaration in include/*.h
+# is exported and bound here.
+P = C.POINTER
+_HIP_SYMBOLS = {
+    "pt_device_count": (C.c_int, [P(C.c_int)]),
+    "pt_create": (C.c_int, [C.c_int, C.c_uint32, C.c_uint32, C.c_uint32, C.c_uint32, P(C.c_void_p)]),
+    "pt_destroy": (None, [C.c_void_p]),
+    "pt_set_scene": (C.c_int, [C.c_void_p, P(PtBvhNode), C.c_uint32, P(PtHittable), C.c_uint32]),
+    "pt_set_texture": (C.c_int, [C.c_void_p, C.c_uint32, P(C.c_float), C.c_uint32, C.c_uint32]),
+    "pt_set_skybox": (C.c_int, [C.c_void_p, C.c_uint32]),
+    "pt_render": (C.c_int, [C.c_void_p, P(PtCamera), C.c_uint32, C.c_uint32, C.c_int, P(C.c_float)]),
+    "pt_render_instrumented": (C.c_int, [C.c_void_p, P(PtCamera), C.c_uint32, C.c_uint32, C.c_int, P(C.c_float),
+                                         P(PtRenderStats)]),
+    "pt_read_accum": (C.c_int, [C.c_void_p, P(C.c_float)]),
+    "pt_copy_accum_device": (C.c_int, [C.c_void_p, C.c_void_p, C.c_size_t]),
+    "pt_tonemap": (C.c_int, [C.c_void_p, C.c_uint32, P(C.c_uint8)]),
+    "pt_read_rng": (C.c_int, [C.c_void_p, P(C.c_uint32)]),
+    "pt_write_rng": (C.c_int, [C.c_void_p, P(C.c_uint32)]),
+    "pt_local_rows": (C.c_uint32, [C.c_void_p]),
+    "pt_last_error": (C.c_char_p, [C.c_void_p]),
+}
+
+_HOST_SYMBOLS = {
+    "pth_last_error": (C.c_char_p, []),
+    "pth_scene_load": (C.c_int, [C.c_char_p, C.c_uint32, C.c_uint32, P(C.c_void_p)]),
+    "pth_scene_free": (None, [C.c_void_p]),
+    "pth_scene_object_count": (C.c_uint32, [C.c_void_p]),
+    "pth_scene_node_count": (C.c_uint32, [C.c_void_p]),
+    "pth_scene_bvh_depth": (C.c_uint32, [C.c_void_p]),
+    "pth_scene_objects": (C.c_int, [C.c_void_p, P(PtHittable), P(C.c_float)]),
+    "pth_scene_bvh": (C.c_int, [C.c_void_p, P(PtBvhNode), P(PtHittable)]),
+    "pth_scene_camera": (C.c_int, [C.c_void_p, P(PtCamera)]),
+    "pth_scene_skybox": (C.c_uint32, [C.c_void_p]),
+    "pth_scene_texture_count": (C.c_uint32, [C.c_void_p]),
+    "pth_scene_texture_info": (C.c_int, [C.c_void_p, C.c_uint32, P(C.c_uint32), P(C.c_uint32)]),
+    "pth_scene_texture_data": (C.c_int, [C.c_void_p, C.c_uint32, P(C.c_float)]),
+    "pth_camera_make": (C.c_int, [P(C.c_float), P(C.c_float), P(C.c_float), C.c_float, C.c_float, P(PtCamera)]),
+    "pth_radians": (C.c_float, [C.c_float]),
+    "pth_renderer_create": (C.c_int, [C.c_uint32, C.c_uint32, C.c_int, C.c_uint32, C.c_uint32, P(C.c_void_p)]),
+    "pth_renderer_destroy": (None, [C.c_void_p]),
+    "pth_renderer_load_scene": (C.c_int, [C.c_void_p, C.c_char_p, P(PtCamera)]),
+    "pth_renderer_render": (C.c_int, [C.c_void_p, P(PtCamera), C.c_uint32, C.c_uint32, C.c_int]),
+    "pth_renderer_timing": (C.c_float, [C.c_void_p]),
+    "pth_renderer_frames": (C.c_uint32, [C.c_void_p]),
+    "pth_renderer_local_rows": (C.c_uint32, [C.c_void_p]),
+    "pth_renderer_hdr": (P(C.c_float), [C.c_void_p]),
+    "pth_renderer_image": (P(C.c_uint8), [C.c_void_p]),
+    "pth_renderer_context": (C.c_void_p, [C.c_void_p]),
+    "pth_write_png": (C.c_int, [C.c_char_p, C.c_uint32, C.c_uint32, P(C.c_uint8), C.c_int]),
+    "pth_write_hdr": (C.c_int, [C.c_char_p, C.c_uint32, C.c_uint32, P(C.c_float), C.c_int]),
+}
+
+_hip = None
+_host = None
+
+
+def _bind(lib: C.CDLL, table: dict) -> C.CDLL:
+    for name, (res, args) in table.items():
+        fn = getattr(lib, name)
+        fn.restype = res
+        fn.argtypes = args
+    return lib
+
+
+def hip() -> C.CDLL:
+    global _hip
+    if _hip is None:
+        if not HIP_LIB.exists():
+            raise RuntimeError(f"{HIP_LIB} is missing: build it with `make` (or __graft_entry__.build())")
+        _hip = _bind(C.CDLL(str(HIP_LIB), mode=C.RTLD_GLOBAL), _HIP_SYMBOLS)
+    return _hip
+
+
+def host() -> C.CDLL:
+    global _host
+    if _host is None:
+        hip()
+        if not HOST_LIB.exists():
+            raise RuntimeError(f"{HOST_LIB} is missing: build it with `make` (or __graft_entry__.build())")
+        _host = _bind(C.CDLL(str(HOST_LIB)), _HOST_SYMBOLS)
+    return _host
+
+
+class PathtracerError(RuntimeError):
+    def __init__(self, code: int, message: str):
+        super().__init__(f"[{code}] {message}")
+        self.code = code
+
+
+def check_host(rc: int) -> None:
+    if rc != PT_OK:
+        raise PathtracerError(rc, (host().pth_last_error() or b"").decode(errors="replace"))
+
+
+def check_ctx(rc: int, ctx) -> None:
+    if rc != PT_OK:
+        raise PathtracerError(rc, (hip().pt_last_error(ctx) or b"").decode(errors="replace"))
+
+
+def device_count() -> int:
+    n = C.c_int(0)
+    hip().pt_device_count(C.byref(n))
+    return int(n.value)

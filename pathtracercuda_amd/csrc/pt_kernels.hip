@@ -1,0 +1,982 @@
+// pt_kernels.hip -- gfx950 path-tracing megakernel, RNG seeding and tonemap kernels, and the C ABI
+// of include/pt_hip.h.
+//
+// Reference behaviour (PathtracerCUDA/src/pathtracer/):
+//   traceKernel  kernels/trace.cu:158-199 (+ getColor :101-156, hitBVH :28-98)
+//   intersection Hittable.inl:88-358, AABB.inl:22-69
+//   shading      Material.inl:20-144, MonteCarlo.h:5-114, brdf.h:4-62
+//   seeding      kernels/initRandState.cu:4-17
+//   tonemap      kernels/tonemap.cu:4-27
+//
+// MI355X design (DESIGN.md has the full rationale):
+//   * one wave64 = one 8x8 pixel tile, one lane = one pixel: the per-pixel XORWOW stream is serial
+//     (SURVEY.md fact 3), so pixels are the only parallel unit;
+//   * the lane runs a flat state machine (segment = traverse + shade) and starts its pixel's next
+//     sample as soon as a path ends, so a wave stays busy until its lanes have finished all
+//     samples of all chunks of the launch, instead of idling at every path end;
+//   * all `chunks` render() calls of the headless loop run in one launch; the per-chunk summation
+//     (color = sum of spp paths, then color + accum) is reproduced exactly in registers;
+//   * RNG state (24 B/pixel) and accum (16 B/pixel) are read once and written once per launch, SoA;
+//   * the BVH node test hoists the per-ray reciprocals (bit-identical to recomputing them) and the
+//     hit record is reconstructed once for the closest hit instead of for every candidate hit.
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+#include <string.h>
+#include <stdio.h>
+#include <string>
+#include <vector>
+#include <algorithm>
+
+#include "pt_math.h"
+#include "../../include/pt_hip.h"
+
+using namespace pt;
+
+namespace {
+
+struct DevTex {
+    const float4* texels;
+    uint32_t width, height;
+    uint32_t pad0, pad1;
+};
+
+struct DevCamera {
+    f3 origin, llc, horizontal, vertical;
+};
+
+struct TraceParams {
+    float4* accum;              // rows x width, local
+    uint32_t* rng;              // 6 planes of rows x width (d, v0..v4)
+    const float4* nodes;        // 2 per node: (min.xyz, max.x), (max.yz, offset bits, pca bits)
+    const float4* prims;        // 4 per prim: row0, row1, row2, (type bits, 0, 0, 0)
+    const float4* mats;         // 3 per prim: (base.xyz, roughness), (emissive.xyz, metal), (tex, type)
+    const DevTex* textures;     // 64 entries
+    unsigned long long* stats;  // 6 counters (instrumented variant only)
+    uint32_t skybox;
+    uint32_t width, height, rowOffset, rowStride, rows;
+    uint32_t spp, chunks, ignoreFirst;
+    uint32_t tilesX, tilesY;
+    DevCamera cam;
+};
+
+// ---------------------------------------------------------------------------------------------
+// texture sampling: CUDA 2-D linear fetch, normalised coordinates, wrap (u) / clamp (v),
+// weights quantised to 1/256 (sampler of Pathtracer.cpp:276-283)
+// ---------------------------------------------------------------------------------------------
+PT_DEV f3 tex2d(const DevTex& t, float u, float v)
+{
+    const float W = (float)t.width, H = (float)t.height;
+    const float uw = u - floorf(u);
+    const float x = uw * W - 0.5f;
+    const float y = v * H - 0.5f;
+    const float fx = floorf(x), fy = floorf(y);
+    float a = x - fx, b = y - fy;
+    a = floorf(a * 256.0f + 0.5f) * (1.0f / 256.0f);
+    b = floorf(b * 256.0f + 0.5f) * (1.0f / 256.0f);
+    const int32_t w = (int32_t)t.width, h = (int32_t)t.height;
+    int32_t i0 = (fx > -1.0e9f && fx < 1.0e9f) ? (int32_t)fx : 0;
+    int32_t j0 = (fy > -1.0e9f && fy < 1.0e9f) ? (int32_t)fy : (fy > 0.0f ? h : -1);
+    int32_t i1 = i0 + 1, j1 = j0 + 1;
+    i0 = ((i0 % w) + w) % w;
+    i1 = ((i1 % w) + w) % w;
+    j0 = j0 < 0 ? 0 : (j0 > h - 1 ? h - 1 : j0);
+    j1 = j1 < 0 ? 0 : (j1 > h - 1 ? h - 1 : j1);
+    const float4 T00 = t.texels[(size_t)j0 * t.width + (size_t)i0];
+    const float4 T10 = t.texels[(size_t)j0 * t.width + (size_t)i1];
+    const float4 T01 = t.texels[(size_t)j1 * t.width + (size_t)i0];
+    const float4 T11 = t.texels[(size_t)j1 * t.width + (size_t)i1];
+    const float w00 = (1.0f - a) * (1.0f - b), w10 = a * (1.0f - b), w01 = (1.0f - a) * b, w11 = a * b;
+    return mk(w00 * T00.x + w10 * T10.x + w01 * T01.x + w11 * T11.x,
+              w00 * T00.y + w10 * T10.y + w01 * T01.y + w11 * T11.y,
+              w00 * T00.z + w10 * T10.z + w01 * T01.z + w11 * T11.z);
+}
+
+// ---------------------------------------------------------------------------------------------
+// intersection
+// ---------------------------------------------------------------------------------------------
+enum : uint32_t { SPHERE = 0, CYLINDER = 1, DISK = 2, CONE = 3, PARABOLOID = 4, QUAD = 5, CUBE = 6 };
+
+struct LocalRay { f3 o, d; };
+
+// Hittable.inl:91-98: world -> object space with the 3x4 inverse rows (origin gets +w)
+PT_DEV LocalRay to_local(const float4& r0, const float4& r1, const float4& r2, f3 o, f3 d)
+{
+    LocalRay l;
+    l.o.x = (o.x * r0.x + o.y * r0.y + o.z * r0.z) + r0.w;
+    l.o.y = (o.x * r1.x + o.y * r1.y + o.z * r1.z) + r1.w;
+    l.o.z = (o.x * r2.x + o.y * r2.y + o.z * r2.z) + r2.w;
+    l.d.x = d.x * r0.x + d.y * r0.y + d.z * r0.z;
+    l.d.y = d.x * r1.x + d.y * r1.y + d.z * r1.z;
+    l.d.z = d.x * r2.x + d.y * r2.y + d.z * r2.z;
+    return l;
+}
+
+// Quadric coefficients of the four quadric shapes (Hittable.inl:152,176,242,273): all have
+// A = C = 1 and D = E = F = G = I = 0; B, H, J vary.  Evaluated with the nonzero terms in the
+// template's order; dropping the exact +-0 terms of D..G and I cannot change a, b or c except for
+// the sign of a zero, which no later operation observes (DESIGN.md "Quadric terms").
+PT_DEV bool quadric_roots(uint32_t type, const LocalRay& r, float& t0, float& t1)
+{
+    const float B = (type == SPHERE) ? 1.0f : (type == CONE ? -1.0f : 0.0f);
+    const float Hc = (type == PARABOLOID) ? -1.0f : 0.0f;
+    const float J = (type == SPHERE || type == CYLINDER) ? -1.0f : 0.0f;
+    const f3 o = r.o, d = r.d;
+    const float a = (d.x * d.x + (B * d.y) * d.y) + d.z * d.z;
+    const float b = (((2.0f * o.x) * d.x + ((2.0f * B) * o.y) * d.y) + (2.0f * o.z) * d.z) + Hc * d.y;
+    const float c = (((o.x * o.x + (B * o.y) * o.y) + o.z * o.z) + Hc * o.y) + J;
+    // quadratic (Hittable.inl:7-39)
+    const float disc = b * b - 4.0f * a * c;
+    if (disc < 0.0f) return false;
+    const float rt = sqrtf(disc);
+    const float q = b < 0.0f ? -0.5f * (b - rt) : -0.5f * (b + rt);
+    float x0 = q / a;
+    float x1 = c / q;
+    t0 = x0 > x1 ? x1 : x0;
+    t1 = x0 > x1 ? x0 : x1;
+    return true;
+}
+
+// Hittable::hit without the hit-record side effects: returns the hit distance of prim `p`.
+PT_DEV bool prim_hit(const float4* __restrict__ prims, uint32_t p, f3 o, f3 d, float tMin, float tMax, float& tOut)
+{
+    const float4 r0 = prims[4 * p + 0];
+    const float4 r1 = prims[4 * p + 1];
+    const float4 r2 = prims[4 * p + 2];
+    const uint32_t type = __float_as_uint(prims[4 * p + 3].x);
+    const LocalRay r = to_local(r0, r1, r2, o, d);
+    if (type == DISK || type == QUAD) {                    // Hittable.inl:205-235, 299-329
+        if (r.d.y == 0.0f) return false;
+        const float t = -r.o.y / r.d.y;
+        if (t <= tMin || t > tMax) return false;
+        const float hx = r.o.x + r.d.x * t;
+        const float hz = r.o.z + r.d.z * t;
+        if (type == QUAD) {
+            if (fabsf(hx) > 1.0f || fabsf(hz) > 1.0f) return false;
+        } else {
+            if ((hx * hx + hz * hz) >= 1.0f) return false;
+        }
+        tOut = t;
+        return true;
+    }
+    if (type == CUBE) {                                     // Hittable.inl:331-358, AABB.inl:46-69
+        float lo = tMin, hi = tMax;
+        const float ox[3] = {r.o.x, r.o.y, r.o.z};
+        const float dx[3] = {r.d.x, r.d.y, r.d.z};
+#pragma unroll
+        for (int a = 0; a < 3; ++a) {
+            const float invD = 1.0f / dx[a];
+            float t0 = (-1.0f - ox[a]) * invD;
+            float t1 = (1.0f - ox[a]) * invD;
+            if (invD < 0.0f) { const float tmp = t0; t0 = t1; t1 = tmp; }
+            lo = t0 > lo ? t0 : lo;
+            hi = t1 < hi ? t1 : hi;
+        }
+        if (hi <= lo) return false;
+        tOut = lo;
+        return true;
+    }
+    float t0 = 0.0f, t1 = 0.0f;                             // quadrics
+    if (!quadric_roots(type, r, t0, t1) || t0 > tMax || t1 <= tMin) return false;
+    if (type == SPHERE) {                                   // Hittable.inl:158 (far-root quirk kept)
+        tOut = t0 > tMin ? t0 : t1;
+        return true;
+    }
+    const float h0 = r.d.y * t0 + r.o.y;                    // Hittable.inl:182-185
+    const float h1 = r.d.y * t1 + r.o.y;
+    const bool v0 = t0 > tMin && t0 <= tMax && h0 >= -1.0f && h0 <= 1.0f;
+    const bool v1 = t1 > tMin && t1 <= tMax && h1 >= -1.0f && h1 <= 1.0f;
+    if (!v0 && !v1) return false;
+    tOut = v0 ? t0 : t1;
+    return true;
+}
+
+struct Counters {
+    uint32_t node_tests, prim_tests, hits, sky, segments, samples;
+};
+
+// hitBVH (trace.cu:28-98): identical visit order, node culling with the current t_max, and
+// in-order leaf tests (later equal-t primitives win).  Returns the closest primitive or ~0u.
+template <bool STATS>
+PT_DEV uint32_t traverse(const float4* __restrict__ nodes, const float4* __restrict__ prims, f3 o, f3 d, float& tHit,
+                         Counters& cnt)
+{
+    const float tMin = 0.001f;
+    float tMax = kFltMax;
+    // AABB.inl:29 recomputes 1/d per node and axis; the value is a function of the ray only.
+    const float ix = 1.0f / d.x, iy = 1.0f / d.y, iz = 1.0f / d.z;
+    // trace.cu:31-36: dirIsNeg from 1/(d != 0 ? d : 1e-7) < 0, i.e. d < 0
+    const bool nx = d.x < 0.0f, ny = d.y < 0.0f, nz = d.z < 0.0f;
+    uint32_t stack[32];
+    uint32_t sp = 0, cur = 0, elem = 0xffffffffu;
+    for (;;) {
+        const float4 A = nodes[2 * cur];
+        const float4 Bq = nodes[2 * cur + 1];
+        if (STATS) cnt.node_tests++;
+        // AABB.inl:22-44, swap-on-negative and the running [tMin, tMax] interval.  The early
+        // returns are dropped: both bounds are monotone and never NaN, so the final test is equal.
+        float lo = tMin, hi = tMax;
+        {
+            float t0 = (A.x - o.x) * ix, t1 = (A.w - o.x) * ix;
+            if (ix < 0.0f) { const float tmp = t0; t0 = t1; t1 = tmp; }
+            lo = t0 > lo ? t0 : lo;
+            hi = t1 < hi ? t1 : hi;
+        }
+        {
+            float t0 = (A.y - o.y) * iy, t1 = (Bq.x - o.y) * iy;
+            if (iy < 0.0f) { const float tmp = t0; t0 = t1; t1 = tmp; }
+            lo = t0 > lo ? t0 : lo;
+            hi = t1 < hi ? t1 : hi;
+        }
+        {
+            float t0 = (A.z - o.z) * iz, t1 = (Bq.y - o.z) * iz;
+            if (iz < 0.0f) { const float tmp = t0; t0 = t1; t1 = tmp; }
+            lo = t0 > lo ? t0 : lo;
+            hi = t1 < hi ? t1 : hi;
+        }
+        const uint32_t offset = __float_as_uint(Bq.z);
+        const uint32_t pca = __float_as_uint(Bq.w);
+        if (hi > lo) {
+            const uint32_t count = pca >> 16;
+            if (count > 0) {
+                for (uint32_t i = 0; i < count; ++i) {
+                    if (STATS) cnt.prim_tests++;
+                    float t;
+                    if (prim_hit(prims, offset + i, o, d, tMin, tMax, t)) {
+                        tMax = t;
+                        elem = offset + i;
+                    }
+                }
+                if (sp == 0) break;
+                cur = stack[--sp];
+            } else {
+                const uint32_t axis = (pca >> 8) & 0xffu;
+                const bool isNeg = axis == 0 ? nx : (axis == 1 ? ny : nz);
+                stack[sp++] = isNeg ? (cur + 1) : offset;
+                cur = isNeg ? offset : (cur + 1);
+            }
+        } else {
+            if (sp == 0) break;
+            cur = stack[--sp];
+        }
+    }
+    tHit = tMax;
+    return elem;
+}
+
+// Surface data of the closest hit (Hittable.inl:126-144 + the shape's normal/uv), rebuilt once.
+struct Surface {
+    f3 p, n;
+    float u, v;
+};
+
+PT_DEV Surface surface_of(const float4* __restrict__ prims, uint32_t e, f3 o, f3 d, float t, bool needUV)
+{
+    const float4 r0 = prims[4 * e + 0];
+    const float4 r1 = prims[4 * e + 1];
+    const float4 r2 = prims[4 * e + 2];
+    const uint32_t type = __float_as_uint(prims[4 * e + 3].x);
+    const LocalRay r = to_local(r0, r1, r2, o, d);
+    const f3 lp = add(r.o, scale(t, r.d));                 // r.at(t) in object space
+    f3 n;
+    float u = 0.0f, v = 0.0f;
+    switch (type) {
+    case SPHERE:
+        n = normalize(lp);
+        if (needUV) {
+            const float theta = acos_(n.y);
+            const float phi = atan2_(n.z, n.x);
+            u = 1.0f - phi / kTwoPi;
+            v = theta / kPi;
+        }
+        break;
+    case CYLINDER:
+        n = mk(lp.x, 0.0f, lp.z);
+        if (needUV) {
+            const float phi = atan2_(n.z, n.x);
+            u = 1.0f - phi / kTwoPi;
+            v = 1.0f - (lp.y * 0.5f + 0.5f);
+        }
+        break;
+    case DISK:
+    case QUAD: {
+        n = mk(0.0f, 1.0f, 0.0f);
+        const float hx = r.o.x + r.d.x * t;
+        const float hz = r.o.z + r.d.z * t;
+        u = hx * 0.5f + 0.5f;
+        v = 1.0f - (hz * 0.5f + 0.5f);
+        break;
+    }
+    case CONE:        // quadricNormal<1,-1,1>: the trailing "+ G/H/I" (int 0) turns -0 into +0
+        n = mk(2.0f * lp.x + 0.0f, 2.0f * (-lp.y) + 0.0f, 2.0f * lp.z + 0.0f);
+        break;
+    case PARABOLOID:  // quadricNormal<1,0,1,0,0,0,0,-1>
+        n = mk(2.0f * lp.x + 0.0f, -1.0f, 2.0f * lp.z + 0.0f);
+        break;
+    default: {        // CUBE: Hittable.inl:345-357
+        const float ax = fabsf(lp.x), ay = fabsf(lp.y), az = fabsf(lp.z);
+        if (ax > ay && ax > az) n = mk(lp.x > 0.0f ? 1.0f : -1.0f, 0.0f, 0.0f);
+        else if (ay > ax && ay > az) n = mk(0.0f, lp.y > 0.0f ? 1.0f : -1.0f, 0.0f);
+        else n = mk(0.0f, 0.0f, lp.z > 0.0f ? 1.0f : -1.0f);
+        break;
+    }
+    }
+    f3 tmp;                                                 // Hittable.inl:131-134
+    tmp.x = n.x * r0.x + n.y * r1.x + n.z * r2.x;
+    tmp.y = n.x * r0.y + n.y * r1.y + n.z * r2.y;
+    tmp.z = n.x * r0.z + n.y * r1.z + n.z * r2.z;
+    Surface s;
+    s.p = add(o, scale(t, d));
+    const f3 on = normalize(tmp);
+    s.n = dot(d, on) < 0.0f ? on : neg(on);                 // HitRecord.h:18-24
+    s.u = u;
+    s.v = v;
+    return s;
+}
+
+// MonteCarlo.h:5-22 tangent frame
+PT_DEV void tangent_frame(f3 N, f3& t, f3& b)
+{
+    const f3 up = fabsf(N.z) < 0.999f ? mk(0.0f, 0.0f, 1.0f) : mk(1.0f, 0.0f, 0.0f);
+    t = normalize(cross(up, N));
+    b = cross(N, t);
+}
+
+PT_DEV f3 cosine_sample(float u0, float u1)   // MonteCarlo.h:24-30
+{
+    const float phi = kTwoPi * u0;
+    const float cosTheta = sqrtf(u1);
+    const float sinTheta = sqrtf(1.0f - u1);
+    float s, c;
+    sincos_pos(phi, s, c);
+    return mk(c * sinTheta, s * sinTheta, cosTheta);
+}
+
+PT_DEV float d_ggx(float NdotH, float a2)     // brdf.h:11-15
+{
+    const float dd = (NdotH * a2 - NdotH) * NdotH + 1.0f;
+    return a2 / (kPi * dd * dd);
+}
+
+PT_DEV f3 vndf_sample(f3 V, float u0, float u1, float a)   // MonteCarlo.h:73-101
+{
+    const f3 Vh = normalize(mk(a * V.x, a * V.y, V.z));
+    const float lensq = Vh.x * Vh.x + Vh.y * Vh.y;
+    const f3 T1 = lensq > 0.0f ? scale(1.0f / sqrtf(lensq), mk(-Vh.y, Vh.x, 0.0f)) : mk(1.0f, 0.0f, 0.0f);
+    const f3 T2 = cross(Vh, T1);
+    const float r = sqrtf(u0);
+    const float phi = kTwoPi * u1;
+    float s, c;
+    sincos_pos(phi, s, c);
+    const float t1 = r * c;
+    float t2 = r * s;
+    const float sv = 0.5f * (1.0f + Vh.z);
+    t2 = (1.0f - sv) * sqrtf(1.0f - t1 * t1) + sv * t2;
+    const f3 Nh = add(add(scale(t1, T1), scale(t2, T2)), scale(sqrtf(clamp01(1.0f - t1 * t1 - t2 * t2)), Vh));
+    return normalize(mk(a * Nh.x, a * Nh.y, clamp01(Nh.z)));
+}
+
+PT_DEV float vndf_pdf(f3 H, f3 V, float a)    // MonteCarlo.h:104-114
+{
+    const float a2 = a * a;
+    const float NdotH = H.z;
+    const float VdotH = clamp01(dot(V, H));
+    const float G1 = (2.0f * V.z) / (V.z + sqrtf(a2 + (1.0f - a2) * (V.z * V.z)));
+    const float Dv = (G1 * VdotH * d_ggx(NdotH, a2)) / V.z;
+    return Dv / (4.0f * VdotH);
+}
+
+PT_DEV f3 specular_ggx(f3 F0, float NdotV, float NdotL, float NdotH, float VdotH, float a2)  // brdf.h:56-62
+{
+    const float D = d_ggx(NdotH, a2);
+    const float lv = NdotL * sqrtf((-NdotV * a2 + NdotV) * NdotV + a2);   // brdf.h:18-24
+    const float ll = NdotV * sqrtf((-NdotL * a2 + NdotL) * NdotL + a2);
+    const float Vis = 0.5f / (lv + ll + 1e-5f);
+    const float v = 1.0f - VdotH;                                          // brdf.h:27-32
+    const float v2 = v * v;
+    const float p = v2 * v2 * v;
+    const f3 F = adds(scale(1.0f - p, F0), p);
+    return scale(D * Vis, F);
+}
+
+template <bool STATS>
+__global__ void __launch_bounds__(256) trace_kernel(TraceParams P)
+{
+    const uint32_t lane = threadIdx.x & 63u;
+    const uint32_t tile = blockIdx.x * 4u + (threadIdx.x >> 6);
+    const uint32_t tileX = tile % P.tilesX, tileY = tile / P.tilesX;
+    const uint32_t px = tileX * 8u + (lane & 7u);
+    const uint32_t ly = tileY * 8u + (lane >> 3);
+    const bool valid = tileY < P.tilesY && px < P.width && ly < P.rows;
+    Counters cnt = {0, 0, 0, 0, 0, 0};
+    if (valid) {
+        const uint32_t py = P.rowOffset + ly * P.rowStride;
+        const size_t npix = (size_t)P.rows * P.width;
+        const size_t li = (size_t)ly * P.width + px;
+        Xorwow rng;
+        rng.d = P.rng[li];
+        rng.v0 = P.rng[npix + li];
+        rng.v1 = P.rng[2 * npix + li];
+        rng.v2 = P.rng[3 * npix + li];
+        rng.v3 = P.rng[4 * npix + li];
+        rng.v4 = P.rng[5 * npix + li];
+        float4 acc = P.accum[li];
+        f3 accum = mk(acc.x, acc.y, acc.z);
+        const float fx = (float)(int32_t)px, fy = (float)(int32_t)py;
+        const float fw = (float)P.width, fh = (float)P.height;
+
+        f3 color = splat(0.0f);       // trace.cu:186 per-chunk sum
+        f3 L = splat(0.0f), T = splat(1.0f);
+        f3 o, d;
+        uint32_t s = 0, c = 0, bounce = 0;
+        bool alive = P.chunks > 0 && P.spp > 0;
+
+        // camera ray of the first sample (trace.cu:190-192, Camera.inl:25-28)
+        {
+            const float u = (fx + uniform(rng)) / fw;
+            const float v = (fy + uniform(rng)) / fh;
+            o = P.cam.origin;
+            d = normalize(add(add(P.cam.llc, scale(u, P.cam.horizontal)), scale(v, P.cam.vertical)));
+        }
+        while (alive) {
+            if (STATS) cnt.segments++;
+            float t;
+            const uint32_t e = traverse<STATS>(P.nodes, P.prims, o, d, t, cnt);
+            bool pathEnd;
+            if (e == 0xffffffffu) {                                       // trace.cu:115-134
+                f3 sky = splat(0.0f);
+                if (P.skybox != 0) {
+                    if (STATS) cnt.sky++;
+                    const float theta = acos_(d.y);
+                    const float phi = atan2_(d.z, d.x);
+                    const float v = theta / kPi;
+                    const float u = phi / kTwoPi;
+                    sky = tex2d(P.textures[P.skybox - 1], u, v);
+                }
+                L = add(L, mul(T, sky));
+                pathEnd = true;
+            } else {
+                if (STATS) cnt.hits++;
+                const float4 m0 = P.mats[3 * e + 0];
+                const float4 m1 = P.mats[3 * e + 1];
+                L = add(L, mul(T, mk(m1.x, m1.y, m1.z)));                 // trace.cu:139
+                if (bounce == 4) {
+                    // 5th segment: its scattered ray is discarded (trace.cu:109), only the two
+                    // uniforms of Material.inl:40-41 are observable.
+                    (void)uniform(rng);
+                    (void)uniform(rng);
+                    pathEnd = true;
+                } else {
+                    const float4 m2 = P.mats[3 * e + 2];
+                    const uint32_t texIdx = __float_as_uint(m2.x);
+                    const uint32_t mtype = __float_as_uint(m2.y);
+                    const Surface sf = surface_of(P.prims, e, o, d, t, texIdx != 0);
+                    f3 tg, bt;
+                    tangent_frame(sf.n, tg, bt);
+                    const f3 wo = neg(d);                                 // MonteCarlo.h:21
+                    const f3 V = normalize(add(add(scale(wo.x, mk(tg.x, bt.x, sf.n.x)), scale(wo.y, mk(tg.y, bt.y, sf.n.y))),
+                                               scale(wo.z, mk(tg.z, bt.z, sf.n.z))));
+                    f3 base = mk(m0.x, m0.y, m0.z);
+                    if (texIdx != 0) {                                    // Material.inl:26-35
+                        const f3 tap = tex2d(P.textures[texIdx - 1], sf.u, sf.v);
+                        base = mk(pow_(tap.x, 2.2f), pow_(tap.y, 2.2f), pow_(tap.z, 2.2f));
+                    }
+                    float rnd0 = uniform(rng);
+                    const float rnd1 = uniform(rng);
+                    const float rough = m0.w, metal = m1.w;
+                    const float a = rough * rough;
+                    const float a2 = a * a;
+                    f3 dir = splat(0.0f), att = splat(0.0f);
+                    float pdf = 0.0f;
+                    bool killed = false;
+                    if (mtype == 0u) {                                    // LAMBERT (Material.inl:67-72)
+                        dir = cosine_sample(rnd0, rnd1);
+                        pdf = dir.z / kPi;
+                        att = scale(kInvPi, base);
+                    } else if (mtype <= 2u) {
+                        bool specular = true;
+                        if (mtype == 2u) {                                // LAMBERT_GGX (:101-144)
+                            if (rnd0 < 0.5f) { rnd0 = 2.0f * rnd0; specular = false; }
+                            else rnd0 = 2.0f * (rnd0 - 0.5f);
+                        }
+                        if (specular) dir = reflect(neg(V), vndf_sample(V, rnd0, rnd1, a));
+                        else dir = cosine_sample(rnd0, rnd1);
+                        if (dir.z < 0.0f) {
+                            killed = true;                                // pdf = 1, attenuation 0
+                        } else {
+                            const float NdotV = fabsf(V.z) + 1e-5f;
+                            const f3 H = normalize(add(V, dir));
+                            const float VdotH = clamp01(dot(V, H));
+                            const float NdotH = clamp01(H.z);
+                            const float NdotL = clamp01(dir.z);
+                            const float ggxPdf = vndf_pdf(H, V, a);
+                            const f3 F0 = lerp(splat(0.04f), base, metal);
+                            const f3 kS = specular_ggx(F0, NdotV, NdotL, NdotH, VdotH, a2);
+                            if (mtype == 1u) {                            // GGX (:74-99)
+                                pdf = ggxPdf;
+                                att = kS;
+                            } else {
+                                const float cosinePdf = dir.z / kPi;
+                                pdf = (ggxPdf + cosinePdf) * 0.5f;
+                                att = add(scale(1.0f - metal, scale(kInvPi, base)), kS);
+                            }
+                        }
+                    }
+                    if (killed || is_zero(att) || pdf == 0.0f) {          // trace.cu:145-148
+                        pathEnd = true;
+                    } else {
+                        // Material.inl:57: normalize(tangentToWorld(...)), which itself normalizes
+                        const f3 sd = normalize(normalize(add(add(scale(dir.x, tg), scale(dir.y, bt)), scale(dir.z, sf.n))));
+                        const f3 w = divs(scale(fabsf(dot(sd, sf.n)), att), pdf);   // trace.cu:150
+                        T = mul(T, w);
+                        o = sf.p;
+                        d = sd;
+                        ++bounce;
+                        pathEnd = false;
+                    }
+                }
+            }
+            if (pathEnd) {
+                color = add(color, L);                                    // trace.cu:193
+                if (STATS) cnt.samples++;
+                if (++s == P.spp) {
+                    const bool ignore = (c == 0) && P.ignoreFirst;       // trace.cu:196
+                    accum = ignore ? color : add(color, accum);
+                    color = splat(0.0f);
+                    s = 0;
+                    if (++c == P.chunks) alive = false;
+                }
+                if (alive) {
+                    const float u = (fx + uniform(rng)) / fw;
+                    const float v = (fy + uniform(rng)) / fh;
+                    o = P.cam.origin;
+                    d = normalize(add(add(P.cam.llc, scale(u, P.cam.horizontal)), scale(v, P.cam.vertical)));
+                    L = splat(0.0f);
+                    T = splat(1.0f);
+                    bounce = 0;
+                }
+            }
+        }
+        if (P.chunks > 0 && P.spp > 0) P.accum[li] = make_float4(accum.x, accum.y, accum.z, 1.0f);
+        P.rng[li] = rng.d;
+        P.rng[npix + li] = rng.v0;
+        P.rng[2 * npix + li] = rng.v1;
+        P.rng[3 * npix + li] = rng.v2;
+        P.rng[4 * npix + li] = rng.v3;
+        P.rng[5 * npix + li] = rng.v4;
+    }
+    if (STATS) {
+        atomicAdd(&P.stats[0], (unsigned long long)cnt.node_tests);
+        atomicAdd(&P.stats[1], (unsigned long long)cnt.prim_tests);
+        atomicAdd(&P.stats[2], (unsigned long long)cnt.hits);
+        atomicAdd(&P.stats[3], (unsigned long long)cnt.sky);
+        atomicAdd(&P.stats[4], (unsigned long long)cnt.segments);
+        atomicAdd(&P.stats[5], (unsigned long long)cnt.samples);
+    }
+}
+
+// initRandState (initRandState.cu:4-17): curand_init(1984 + x + y * width, 0, 0)
+__global__ void __launch_bounds__(256) init_rng_kernel(uint32_t* rng, uint32_t width, uint32_t rows, uint32_t rowOffset,
+                                                       uint32_t rowStride)
+{
+    const size_t npix = (size_t)rows * width;
+    const size_t li = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (li >= npix) return;
+    const uint32_t x = (uint32_t)(li % width);
+    const uint32_t ly = (uint32_t)(li / width);
+    const uint32_t y = rowOffset + ly * rowStride;
+    const uint32_t idx = x + y * width;
+    const Xorwow s = xorwow_init((uint64_t)(uint32_t)(1984u + idx));
+    rng[li] = s.d;
+    rng[npix + li] = s.v0;
+    rng[2 * npix + li] = s.v1;
+    rng[3 * npix + li] = s.v2;
+    rng[4 * npix + li] = s.v3;
+    rng[5 * npix + li] = s.v4;
+}
+
+// tonemap (tonemap.cu:4-27)
+__global__ void __launch_bounds__(256) tonemap_kernel(uchar4* out, const float4* accum, size_t npix, uint32_t frames)
+{
+    const size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= npix) return;
+    const float4 a = accum[i];
+    f3 c = divs(mk(a.x, a.y, a.z), (float)frames);
+    c = mul(mk(1.0f / (c.x + 1.0f), 1.0f / (c.y + 1.0f), 1.0f / (c.z + 1.0f)), c);
+    const float g = 1.0f / 2.2f;
+    const float ch[3] = {pow_(c.x, g), pow_(c.y, g), pow_(c.z, g)};
+    unsigned char q[3];
+#pragma unroll
+    for (int k = 0; k < 3; ++k) {
+        const float f = ch[k] * 255.0f;
+        const int32_t v = (f != f) ? 0 : f2i_x86(f);
+        q[k] = (unsigned char)(v & 0xff);
+    }
+    out[i] = make_uchar4(q[0], q[1], q[2], 255);
+}
+
+} // namespace
+
+// =============================================================================================
+// C ABI
+// =============================================================================================
+struct pt_context {
+    int device = 0;
+    hipStream_t stream = nullptr;
+    hipEvent_t ev0 = nullptr, ev1 = nullptr;
+    uint32_t width = 0, height = 0, rowOffset = 0, rowStride = 1, rows = 0;
+    float4* accum = nullptr;
+    uint32_t* rng = nullptr;
+    float4* nodes = nullptr;
+    float4* prims = nullptr;
+    float4* mats = nullptr;
+    uint32_t nodeCount = 0, primCount = 0;
+    DevTex* texTable = nullptr;
+    DevTex hostTex[PT_MAX_TEXTURES] = {};
+    uint32_t skybox = 0;
+    unsigned long long* stats = nullptr;
+    std::string err;
+};
+
+#define PT_HIP_CHECK(ctx, expr)                                                              \
+    do {                                                                                     \
+        hipError_t e_ = (expr);                                                              \
+        if (e_ != hipSuccess) {                                                              \
+            if (ctx) {                                                                       \
+                char b_[512];                                                                \
+                snprintf(b_, sizeof(b_), "HIP error = %u (%s) at %s:%d '%s'", (unsigned)e_,  \
+                         hipGetErrorString(e_), __FILE__, __LINE__, #expr);                  \
+                (ctx)->err = b_;                                                             \
+            }                                                                                \
+            return PT_ERR_HIP;                                                               \
+        }                                                                                    \
+    } while (0)
+
+static inline float u2f(uint32_t u)
+{
+    float f;
+    memcpy(&f, &u, 4);
+    return f;
+}
+
+static inline f3 hf3(const float* v) { f3 r; r.x = v[0]; r.y = v[1]; r.z = v[2]; return r; }
+
+static int fail(pt_context* ctx, int code, const char* msg)
+{
+    if (ctx) ctx->err = msg;
+    return code;
+}
+
+extern "C" {
+
+PT_API int pt_device_count(int* count)
+{
+    if (!count) return PT_ERR_ARG;
+    int n = 0;
+    if (hipGetDeviceCount(&n) != hipSuccess) n = 0;
+    *count = n;
+    return PT_OK;
+}
+
+PT_API int pt_create(int device, uint32_t width, uint32_t height, uint32_t row_offset, uint32_t row_stride,
+                     pt_context** out)
+{
+    if (!out || width == 0 || height == 0 || row_stride == 0) return PT_ERR_ARG;
+    *out = nullptr;
+    int n = 0;
+    if (hipGetDeviceCount(&n) != hipSuccess || n == 0) return PT_ERR_NO_DEVICE;
+    if (device < 0 || device >= n) return PT_ERR_ARG;
+    pt_context* ctx = new pt_context();
+    ctx->device = device;
+    ctx->width = width;
+    ctx->height = height;
+    ctx->rowOffset = row_offset;
+    ctx->rowStride = row_stride;
+    ctx->rows = row_offset < height ? (height - row_offset + row_stride - 1) / row_stride : 0;
+    auto bail = [&](int code) { pt_destroy(ctx); return code; };
+    if (hipSetDevice(device) != hipSuccess) return bail(PT_ERR_HIP);
+    if (hipStreamCreateWithFlags(&ctx->stream, hipStreamNonBlocking) != hipSuccess) return bail(PT_ERR_HIP);
+    if (hipEventCreate(&ctx->ev0) != hipSuccess || hipEventCreate(&ctx->ev1) != hipSuccess) return bail(PT_ERR_HIP);
+    const size_t npix = (size_t)ctx->rows * width;
+    const size_t nalloc = npix ? npix : 1;
+    if (hipMalloc(&ctx->accum, nalloc * sizeof(float4)) != hipSuccess) return bail(PT_ERR_HIP);
+    if (hipMalloc(&ctx->rng, nalloc * 6 * sizeof(uint32_t)) != hipSuccess) return bail(PT_ERR_HIP);
+    if (hipMalloc(&ctx->texTable, PT_MAX_TEXTURES * sizeof(DevTex)) != hipSuccess) return bail(PT_ERR_HIP);
+    if (hipMalloc(&ctx->stats, 8 * sizeof(unsigned long long)) != hipSuccess) return bail(PT_ERR_HIP);
+    if (hipMemsetAsync(ctx->accum, 0, nalloc * sizeof(float4), ctx->stream) != hipSuccess) return bail(PT_ERR_HIP);
+    if (hipMemcpyAsync(ctx->texTable, ctx->hostTex, sizeof(ctx->hostTex), hipMemcpyHostToDevice, ctx->stream) != hipSuccess)
+        return bail(PT_ERR_HIP);
+    if (npix) {
+        const unsigned blocks = (unsigned)((npix + 255) / 256);
+        init_rng_kernel<<<blocks, 256, 0, ctx->stream>>>(ctx->rng, width, ctx->rows, row_offset, row_stride);
+        if (hipGetLastError() != hipSuccess) return bail(PT_ERR_HIP);
+    }
+    if (hipStreamSynchronize(ctx->stream) != hipSuccess) return bail(PT_ERR_HIP);
+    *out = ctx;
+    return PT_OK;
+}
+
+PT_API void pt_destroy(pt_context* ctx)
+{
+    if (!ctx) return;
+    (void)hipSetDevice(ctx->device);
+    if (ctx->stream) (void)hipStreamSynchronize(ctx->stream);
+    (void)hipFree(ctx->accum);
+    (void)hipFree(ctx->rng);
+    (void)hipFree(ctx->nodes);
+    (void)hipFree(ctx->prims);
+    (void)hipFree(ctx->mats);
+    (void)hipFree(ctx->texTable);
+    (void)hipFree(ctx->stats);
+    for (auto& t : ctx->hostTex) (void)hipFree((void*)t.texels);
+    if (ctx->ev0) (void)hipEventDestroy(ctx->ev0);
+    if (ctx->ev1) (void)hipEventDestroy(ctx->ev1);
+    if (ctx->stream) (void)hipStreamDestroy(ctx->stream);
+    delete ctx;
+}
+
+// Host-side validation of the BVH so a malformed scene can never make the kernel read out of
+// bounds or overflow its 32-entry stack (the reference does not check, trace.cu:39).
+static int validate_scene(pt_context* ctx, const pt_bvh_node* nodes, uint32_t nn, const pt_hittable* prims, uint32_t np)
+{
+    for (uint32_t i = 0; i < np; ++i) {
+        if (prims[i].type > 6u) return fail(ctx, PT_ERR_ARG, "pt_set_scene: invalid hittable type");
+        if (prims[i].texture_index > PT_MAX_TEXTURES) return fail(ctx, PT_ERR_ARG, "pt_set_scene: invalid texture index");
+    }
+    // iterative DFS computing the depth (number of nodes on the root-to-node path)
+    std::vector<std::pair<uint32_t, uint32_t>> st;
+    st.push_back({0u, 1u});
+    uint32_t maxDepth = 0, visited = 0;
+    while (!st.empty()) {
+        auto [i, depth] = st.back();
+        st.pop_back();
+        if (i >= nn) return fail(ctx, PT_ERR_ARG, "pt_set_scene: node index out of range");
+        if (++visited > nn) return fail(ctx, PT_ERR_ARG, "pt_set_scene: BVH is not a tree");
+        maxDepth = std::max(maxDepth, depth);
+        const uint32_t pca = nodes[i].primitive_count_axis;
+        const uint32_t count = pca >> 16;
+        if (count > 0) {
+            if ((uint64_t)nodes[i].offset + count > np) return fail(ctx, PT_ERR_ARG, "pt_set_scene: leaf range out of bounds");
+        } else {
+            if (((pca >> 8) & 0xffu) > 2u) return fail(ctx, PT_ERR_ARG, "pt_set_scene: invalid split axis");
+            if (nodes[i].offset <= i + 1 || nodes[i].offset >= nn || i + 1 >= nn)
+                return fail(ctx, PT_ERR_ARG, "pt_set_scene: invalid child index");
+            st.push_back({i + 1, depth + 1});
+            st.push_back({nodes[i].offset, depth + 1});
+        }
+    }
+    if (maxDepth > 33) return fail(ctx, PT_ERR_DEPTH, "pt_set_scene: BVH depth exceeds the 32-entry traversal stack");
+    return PT_OK;
+}
+
+PT_API int pt_set_scene(pt_context* ctx, const pt_bvh_node* nodes, uint32_t node_count, const pt_hittable* prims,
+                        uint32_t prim_count)
+{
+    if (!ctx) return PT_ERR_ARG;
+    if (node_count == 0 || prim_count == 0 || !nodes || !prims) return fail(ctx, PT_ERR_ARG, "pt_set_scene: empty scene");
+    int rc = validate_scene(ctx, nodes, node_count, prims, prim_count);
+    if (rc != PT_OK) return rc;
+    std::vector<float4> hn(2 * (size_t)node_count), hp(4 * (size_t)prim_count), hm(3 * (size_t)prim_count);
+    for (uint32_t i = 0; i < node_count; ++i) {
+        const pt_bvh_node& n = nodes[i];
+        hn[2 * i] = make_float4(n.aabb_min[0], n.aabb_min[1], n.aabb_min[2], n.aabb_max[0]);
+        hn[2 * i + 1] = make_float4(n.aabb_max[1], n.aabb_max[2], u2f(n.offset),
+                                    u2f(n.primitive_count_axis));
+    }
+    for (uint32_t i = 0; i < prim_count; ++i) {
+        const pt_hittable& h = prims[i];
+        for (int r = 0; r < 3; ++r)
+            hp[4 * i + r] = make_float4(h.inv_transform_rows[r][0], h.inv_transform_rows[r][1], h.inv_transform_rows[r][2],
+                                        h.inv_transform_rows[r][3]);
+        hp[4 * i + 3] = make_float4(u2f(h.type), 0.0f, 0.0f, 0.0f);
+        hm[3 * i] = make_float4(h.base_color[0], h.base_color[1], h.base_color[2], h.roughness);
+        hm[3 * i + 1] = make_float4(h.emissive[0], h.emissive[1], h.emissive[2], h.metalness);
+        hm[3 * i + 2] = make_float4(u2f(h.texture_index), u2f(h.material_type), 0.0f, 0.0f);
+    }
+    PT_HIP_CHECK(ctx, hipSetDevice(ctx->device));
+    PT_HIP_CHECK(ctx, hipStreamSynchronize(ctx->stream));
+    (void)hipFree(ctx->nodes);
+    (void)hipFree(ctx->prims);
+    (void)hipFree(ctx->mats);
+    ctx->nodes = ctx->prims = ctx->mats = nullptr;
+    ctx->nodeCount = ctx->primCount = 0;
+    PT_HIP_CHECK(ctx, hipMalloc(&ctx->nodes, hn.size() * sizeof(float4)));
+    PT_HIP_CHECK(ctx, hipMalloc(&ctx->prims, hp.size() * sizeof(float4)));
+    PT_HIP_CHECK(ctx, hipMalloc(&ctx->mats, hm.size() * sizeof(float4)));
+    PT_HIP_CHECK(ctx, hipMemcpy(ctx->nodes, hn.data(), hn.size() * sizeof(float4), hipMemcpyHostToDevice));
+    PT_HIP_CHECK(ctx, hipMemcpy(ctx->prims, hp.data(), hp.size() * sizeof(float4), hipMemcpyHostToDevice));
+    PT_HIP_CHECK(ctx, hipMemcpy(ctx->mats, hm.data(), hm.size() * sizeof(float4), hipMemcpyHostToDevice));
+    ctx->nodeCount = node_count;
+    ctx->primCount = prim_count;
+    return PT_OK;
+}
+
+PT_API int pt_set_texture(pt_context* ctx, uint32_t handle, const float* rgba, uint32_t width, uint32_t height)
+{
+    if (!ctx) return PT_ERR_ARG;
+    if (handle == 0 || handle > PT_MAX_TEXTURES || !rgba || width == 0 || height == 0)
+        return fail(ctx, PT_ERR_ARG, "pt_set_texture: invalid argument");
+    PT_HIP_CHECK(ctx, hipSetDevice(ctx->device));
+    PT_HIP_CHECK(ctx, hipStreamSynchronize(ctx->stream));
+    DevTex& t = ctx->hostTex[handle - 1];
+    (void)hipFree((void*)t.texels);
+    t = DevTex{};
+    float4* mem = nullptr;
+    const size_t bytes = (size_t)width * height * sizeof(float4);
+    PT_HIP_CHECK(ctx, hipMalloc(&mem, bytes));
+    PT_HIP_CHECK(ctx, hipMemcpy(mem, rgba, bytes, hipMemcpyHostToDevice));
+    t.texels = mem;
+    t.width = width;
+    t.height = height;
+    PT_HIP_CHECK(ctx, hipMemcpy(ctx->texTable, ctx->hostTex, sizeof(ctx->hostTex), hipMemcpyHostToDevice));
+    return PT_OK;
+}
+
+PT_API int pt_set_skybox(pt_context* ctx, uint32_t handle)
+{
+    if (!ctx) return PT_ERR_ARG;
+    if (handle > PT_MAX_TEXTURES) return fail(ctx, PT_ERR_ARG, "pt_set_skybox: invalid handle");
+    ctx->skybox = handle;
+    return PT_OK;
+}
+
+static int render_impl(pt_context* ctx, const pt_camera* cam, uint32_t spp, uint32_t chunks, int ignore, float* gpu_ms,
+                       pt_render_stats* stats)
+{
+    if (!ctx || !cam) return PT_ERR_ARG;
+    if (gpu_ms) *gpu_ms = 0.0f;
+    if (stats) memset(stats, 0, sizeof(*stats));
+    PT_HIP_CHECK(ctx, hipSetDevice(ctx->device));
+    if (ctx->nodeCount < 1 || ctx->primCount < 1 || spp == 0 || chunks == 0 || ctx->rows == 0) return PT_OK;
+    // textures referenced by the launch must exist (the reference would read an invalid object)
+    if (ctx->skybox != 0 && ctx->hostTex[ctx->skybox - 1].texels == nullptr)
+        return fail(ctx, PT_ERR_STATE, "pt_render: skybox handle has no texture");
+    TraceParams P;
+    memset(&P, 0, sizeof(P));
+    P.accum = ctx->accum;
+    P.rng = ctx->rng;
+    P.nodes = ctx->nodes;
+    P.prims = ctx->prims;
+    P.mats = ctx->mats;
+    P.textures = ctx->texTable;
+    P.stats = ctx->stats;
+    P.skybox = ctx->skybox;
+    P.width = ctx->width;
+    P.height = ctx->height;
+    P.rowOffset = ctx->rowOffset;
+    P.rowStride = ctx->rowStride;
+    P.rows = ctx->rows;
+    P.spp = spp;
+    P.chunks = chunks;
+    P.ignoreFirst = ignore ? 1u : 0u;
+    P.tilesX = (ctx->width + 7) / 8;
+    P.tilesY = (ctx->rows + 7) / 8;
+    P.cam.origin = hf3(cam->origin);
+    P.cam.llc = hf3(cam->lower_left_corner);
+    P.cam.horizontal = hf3(cam->horizontal);
+    P.cam.vertical = hf3(cam->vertical);
+    const uint32_t tiles = P.tilesX * P.tilesY;
+    const unsigned blocks = (tiles + 3) / 4;
+    if (stats) PT_HIP_CHECK(ctx, hipMemsetAsync(ctx->stats, 0, 8 * sizeof(unsigned long long), ctx->stream));
+    PT_HIP_CHECK(ctx, hipEventRecord(ctx->ev0, ctx->stream));
+    if (stats) trace_kernel<true><<<blocks, 256, 0, ctx->stream>>>(P);
+    else trace_kernel<false><<<blocks, 256, 0, ctx->stream>>>(P);
+    PT_HIP_CHECK(ctx, hipGetLastError());
+    PT_HIP_CHECK(ctx, hipEventRecord(ctx->ev1, ctx->stream));
+    PT_HIP_CHECK(ctx, hipEventSynchronize(ctx->ev1));
+    float ms = 0.0f;
+    PT_HIP_CHECK(ctx, hipEventElapsedTime(&ms, ctx->ev0, ctx->ev1));
+    if (gpu_ms) *gpu_ms = ms;
+    if (stats) {
+        unsigned long long h[8];
+        PT_HIP_CHECK(ctx, hipMemcpy(h, ctx->stats, sizeof(h), hipMemcpyDeviceToHost));
+        stats->node_tests = h[0];
+        stats->prim_tests = h[1];
+        stats->hits = h[2];
+        stats->sky_lookups = h[3];
+        stats->segments = h[4];
+        stats->samples = h[5];
+    }
+    return PT_OK;
+}
+
+PT_API int pt_render(pt_context* ctx, const pt_camera* camera, uint32_t spp, uint32_t chunks, int ignore_history,
+                     float* gpu_ms)
+{
+    return render_impl(ctx, camera, spp, chunks, ignore_history, gpu_ms, nullptr);
+}
+
+PT_API int pt_render_instrumented(pt_context* ctx, const pt_camera* camera, uint32_t spp, uint32_t chunks, int ignore_history,
+                           float* gpu_ms, pt_render_stats* stats)
+{
+    if (!stats) return PT_ERR_ARG;
+    return render_impl(ctx, camera, spp, chunks, ignore_history, gpu_ms, stats);
+}
+
+PT_API int pt_read_accum(pt_context* ctx, float* dst)
+{
+    if (!ctx || !dst) return PT_ERR_ARG;
+    PT_HIP_CHECK(ctx, hipSetDevice(ctx->device));
+    PT_HIP_CHECK(ctx, hipStreamSynchronize(ctx->stream));
+    PT_HIP_CHECK(ctx, hipMemcpy(dst, ctx->accum, (size_t)ctx->rows * ctx->width * sizeof(float4), hipMemcpyDeviceToHost));
+    return PT_OK;
+}
+
+PT_API int pt_copy_accum_device(pt_context* ctx, void* dst_device, size_t bytes)
+{
+    if (!ctx || !dst_device) return PT_ERR_ARG;
+    const size_t need = (size_t)ctx->rows * ctx->width * sizeof(float4);
+    if (bytes < need) return fail(ctx, PT_ERR_ARG, "pt_copy_accum_device: destination too small");
+    PT_HIP_CHECK(ctx, hipSetDevice(ctx->device));
+    PT_HIP_CHECK(ctx, hipMemcpyAsync(dst_device, ctx->accum, need, hipMemcpyDeviceToDevice, ctx->stream));
+    PT_HIP_CHECK(ctx, hipStreamSynchronize(ctx->stream));
+    return PT_OK;
+}
+
+PT_API int pt_tonemap(pt_context* ctx, uint32_t frames, uint8_t* dst)
+{
+    if (!ctx || !dst) return PT_ERR_ARG;
+    PT_HIP_CHECK(ctx, hipSetDevice(ctx->device));
+    const size_t npix = (size_t)ctx->rows * ctx->width;
+    if (npix == 0) return PT_OK;
+    uchar4* out = nullptr;
+    PT_HIP_CHECK(ctx, hipMalloc(&out, npix * sizeof(uchar4)));
+    tonemap_kernel<<<(unsigned)((npix + 255) / 256), 256, 0, ctx->stream>>>(out, ctx->accum, npix, frames);
+    hipError_t e = hipGetLastError();
+    if (e == hipSuccess) e = hipMemcpyAsync(dst, out, npix * sizeof(uchar4), hipMemcpyDeviceToHost, ctx->stream);
+    if (e == hipSuccess) e = hipStreamSynchronize(ctx->stream);
+    (void)hipFree(out);
+    PT_HIP_CHECK(ctx, e);
+    return PT_OK;
+}
+
+PT_API int pt_read_rng(pt_context* ctx, uint32_t* dst)
+{
+    if (!ctx || !dst) return PT_ERR_ARG;
+    PT_HIP_CHECK(ctx, hipSetDevice(ctx->device));
+    PT_HIP_CHECK(ctx, hipStreamSynchronize(ctx->stream));
+    const size_t npix = (size_t)ctx->rows * ctx->width;
+    std::vector<uint32_t> soa(6 * npix);
+    PT_HIP_CHECK(ctx, hipMemcpy(soa.data(), ctx->rng, soa.size() * sizeof(uint32_t), hipMemcpyDeviceToHost));
+    for (size_t i = 0; i < npix; ++i)
+        for (int k = 0; k < 6; ++k) dst[6 * i + k] = soa[k * npix + i];
+    return PT_OK;
+}
+
+PT_API int pt_write_rng(pt_context* ctx, const uint32_t* src)
+{
+    if (!ctx || !src) return PT_ERR_ARG;
+    PT_HIP_CHECK(ctx, hipSetDevice(ctx->device));
+    PT_HIP_CHECK(ctx, hipStreamSynchronize(ctx->stream));
+    const size_t npix = (size_t)ctx->rows * ctx->width;
+    std::vector<uint32_t> soa(6 * npix);
+    for (size_t i = 0; i < npix; ++i)
+        for (int k = 0; k < 6; ++k) soa[k * npix + i] = src[6 * i + k];
+    PT_HIP_CHECK(ctx, hipMemcpy(ctx->rng, soa.data(), soa.size() * sizeof(uint32_t), hipMemcpyHostToDevice));
+    return PT_OK;
+}
+
+PT_API uint32_t pt_local_rows(const pt_context* ctx) { return ctx ? ctx->rows : 0; }
+
+PT_API const char* pt_last_error(const pt_context* ctx) { return ctx ? ctx->err.c_str() : "null context"; }
+
+} // extern "C"

@@ -1,0 +1,234 @@
+// pt_math.h -- device float math for the gfx950 path-tracing megakernel.
+//
+// Semantics follow the reference's __host__ __device__ headers operation for operation
+// (PathtracerCUDA/src/pathtracer/vec3.inl, MonteCarlo.h, brdf.h): every division, the order of
+// every sum, and the reciprocal-multiply forms (vec3 / s == (1/s) * v, vec3.inl:116-119) are kept,
+// because one ulp anywhere can flip a hit/miss and decorrelate a pixel's RNG stream.  Compiled with
+// -ffp-contract=off; hipcc's default IEEE division and sqrt are used (correctly rounded).
+//
+// The transcendentals are this project's own single-precision routines (Cephes-style reduction +
+// minimax polynomials, no FMA): CUDA libdevice is not available on AMD and ocml's results differ
+// in the last ulp, so the path fixes one definition of sinf/cosf/acosf/atan2f/powf (DESIGN.md
+// "Float determinism").
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#define PT_DEV __device__ __forceinline__
+
+namespace pt {
+
+constexpr float kPi = 3.14159265358979323846f;   // vec3.h:5
+constexpr float kTwoPi = 2.0f * kPi;             // folded exactly as `2.0f * PI`
+constexpr float kInvPi = 1.0f / kPi;             // brdf.h:53 `1.0f / PI`
+constexpr float kFltMax = 3.402823466e+38f;
+
+struct f3 { float x, y, z; };
+
+PT_DEV f3 mk(float x, float y, float z) { return f3{x, y, z}; }
+PT_DEV f3 splat(float s) { return f3{s, s, s}; }
+PT_DEV f3 neg(f3 a) { return f3{-a.x, -a.y, -a.z}; }
+PT_DEV f3 add(f3 a, f3 b) { return f3{a.x + b.x, a.y + b.y, a.z + b.z}; }
+PT_DEV f3 adds(f3 a, float s) { return f3{a.x + s, a.y + s, a.z + s}; }
+PT_DEV f3 sub(f3 a, f3 b) { return f3{a.x - b.x, a.y - b.y, a.z - b.z}; }
+PT_DEV f3 mul(f3 a, f3 b) { return f3{a.x * b.x, a.y * b.y, a.z * b.z}; }
+PT_DEV f3 scale(float t, f3 v) { return f3{t * v.x, t * v.y, t * v.z}; }
+PT_DEV f3 divs(f3 v, float t) { return scale(1.0f / t, v); }
+PT_DEV float dot(f3 u, f3 v) { return u.x * v.x + u.y * v.y + u.z * v.z; }
+PT_DEV f3 cross(f3 u, f3 v) { return f3{u.y * v.z - u.z * v.y, u.z * v.x - u.x * v.z, u.x * v.y - u.y * v.x}; }
+PT_DEV float length(f3 v) { return sqrtf(v.x * v.x + v.y * v.y + v.z * v.z); }
+PT_DEV f3 normalize(f3 v) { return divs(v, length(v)); }
+PT_DEV f3 reflect(f3 v, f3 n) { return sub(v, scale(2.0f * dot(v, n), n)); }
+PT_DEV f3 lerp(f3 x, f3 y, float a) { return add(scale(1.0f - a, x), scale(a, y)); }
+PT_DEV float clamp01(float x) { x = x < 0.0f ? 0.0f : x; x = x > 1.0f ? 1.0f : x; return x; }
+PT_DEV bool is_zero(f3 a) { return a.x == 0.0f && a.y == 0.0f && a.z == 0.0f; }
+
+// ---------------------------------------------------------------------------------------------
+// transcendentals (same algorithm, constants and evaluation order as the oracle restatement)
+// ---------------------------------------------------------------------------------------------
+constexpr float kFopi = 1.27323954473516f;
+constexpr float kDp1 = 0.78515625f;
+constexpr float kDp2 = 2.4187564849853515625e-4f;
+constexpr float kDp3 = 3.77489497744594108e-8f;
+constexpr float kPio2 = 1.5707963267948966192f;
+constexpr float kPio4 = 0.7853981633974483096f;
+
+PT_DEV float sin_poly(float z, float zz)
+{
+    return ((-1.9515295891E-4f * zz + 8.3321608736E-3f) * zz - 1.6666654611E-1f) * zz * z + z;
+}
+PT_DEV float cos_poly(float zz)
+{
+    float y = ((2.443315711809948E-5f * zz - 1.388731625493765E-3f) * zz + 4.166664568298827E-2f) * zz * zz;
+    y = y - 0.5f * zz;
+    return y + 1.0f;
+}
+
+// sin and cos of one argument x in [0, 65536] (both call sites pass 2*pi*u, u in (0,1]).
+PT_DEV void sincos_pos(float x, float& s, float& c)
+{
+    int32_t j = (int32_t)(x * kFopi);
+    float y = (float)j;
+    if (j & 1) { j += 1; y += 1.0f; }
+    j &= 7;
+    bool sneg = false, cneg = false;
+    if (j > 3) { sneg = true; cneg = true; j -= 4; }
+    if (j > 1) cneg = !cneg;
+    const float z = ((x - y * kDp1) - y * kDp2) - y * kDp3;
+    const float zz = z * z;
+    const float ps = sin_poly(z, zz);
+    const float pc = cos_poly(zz);
+    const bool swap = (j == 1 || j == 2);
+    float rs = swap ? pc : ps;
+    float rc = swap ? ps : pc;
+    s = sneg ? -rs : rs;
+    c = cneg ? -rc : rc;
+}
+
+PT_DEV float asin_core(float a)
+{
+    float x, z;
+    bool flag;
+    if (a > 0.5f) { z = 0.5f * (1.0f - a); x = sqrtf(z); flag = true; }
+    else { x = a; z = x * x; flag = false; }
+    float r;
+    if (a < 1.0e-4f) r = a;
+    else r = ((((4.2163199048E-2f * z + 2.4181311049E-2f) * z + 4.5470025998E-2f) * z + 7.4953002686E-2f) * z
+              + 1.6666752422E-1f) * z * x + x;
+    if (flag) { r = r + r; r = kPio2 - r; }
+    return r;
+}
+
+PT_DEV float acos_(float x)
+{
+    if (!(x >= -1.0f && x <= 1.0f)) return (x != x) ? x : __uint_as_float(0x7fc00000u);
+    if (x < -0.5f) return kPi - 2.0f * asin_core(sqrtf(0.5f * (1.0f + x)));
+    if (x > 0.5f) return 2.0f * asin_core(sqrtf(0.5f * (1.0f - x)));
+    float r = asin_core(fabsf(x));
+    return x < 0.0f ? kPio2 + r : kPio2 - r;
+}
+
+PT_DEV float atan_pos(float x)
+{
+    float y;
+    if (x > 2.414213562373095f) { y = kPio2; x = -1.0f / x; }
+    else if (x > 0.4142135623730950f) { y = kPio4; x = (x - 1.0f) / (x + 1.0f); }
+    else y = 0.0f;
+    const float z = x * x;
+    return y + ((((8.05374449538e-2f * z - 1.38776856032E-1f) * z + 1.99777106478E-1f) * z - 3.33329491539E-1f) * z * x + x);
+}
+
+PT_DEV float atan2_(float y, float x)
+{
+    if (x != x || y != y) return x + y;
+    if (y == 0.0f) {
+        if (__float_as_uint(x) >> 31) return (__float_as_uint(y) >> 31) ? -kPi : kPi;
+        return y;
+    }
+    if (x == 0.0f) return y < 0.0f ? -kPio2 : kPio2;
+    const float ay = fabsf(y), ax = fabsf(x);
+    if (__builtin_isinf(ax)) {
+        float r;
+        if (__builtin_isinf(ay)) r = (x > 0.0f) ? kPio4 : 3.0f * kPio4;
+        else r = (x > 0.0f) ? 0.0f : kPi;
+        return y < 0.0f ? -r : r;
+    }
+    float r = atan_pos(ay / ax);
+    if (x < 0.0f) r = kPi - r;
+    return y < 0.0f ? -r : r;
+}
+
+PT_DEV float log_(float x)
+{
+    uint32_t b = __float_as_uint(x);
+    int32_t e = 0;
+    if ((b >> 23) == 0) { x = x * 8388608.0f; b = __float_as_uint(x); e = -23; }
+    e += (int32_t)((b >> 23) & 0xffu) - 126;
+    x = __uint_as_float((b & 0x807fffffu) | 0x3f000000u);
+    if (x < 0.707106781186547524f) { e -= 1; x = x + x - 1.0f; }
+    else x = x - 1.0f;
+    float z = x * x;
+    float y = ((((((((7.0376836292E-2f * x - 1.1514610310E-1f) * x + 1.1676998740E-1f) * x - 1.2420140846E-1f) * x
+                   + 1.4249322787E-1f) * x - 1.6668057665E-1f) * x + 2.0000714765E-1f) * x - 2.4999993993E-1f) * x
+              + 3.3333331174E-1f) * x * z;
+    const float fe = (float)e;
+    y = y + -2.12194440e-4f * fe;
+    y = y + -0.5f * z;
+    z = x + y;
+    z = z + 0.693359375f * fe;
+    return z;
+}
+
+PT_DEV float exp_(float x)
+{
+    if (x > 88.7228391f) return __uint_as_float(0x7f800000u);
+    if (x < -103.972084f) return 0.0f;
+    float z = floorf(1.44269504088896341f * x + 0.5f);
+    x = x - z * 0.693359375f;
+    x = x - z * -2.12194440e-4f;
+    const int32_t n = (int32_t)z;
+    z = x * x;
+    float r = (((((1.9875691500E-4f * x + 1.3981999507E-3f) * x + 8.3334519073E-3f) * x + 4.1665795894E-2f) * x
+                + 1.6666665459E-1f) * x + 5.0000001201E-1f) * z + x + 1.0f;
+    const int32_t n1 = n / 2, n2 = n - n1;
+    r = r * __uint_as_float((uint32_t)(n1 + 127) << 23);
+    r = r * __uint_as_float((uint32_t)(n2 + 127) << 23);
+    return r;
+}
+
+PT_DEV float pow_(float x, float y)
+{
+    if (x != x || y != y) return x + y;
+    if (y == 0.0f || x == 1.0f) return 1.0f;
+    if (x == 0.0f) return y > 0.0f ? 0.0f : __uint_as_float(0x7f800000u);
+    if (x < 0.0f) return __uint_as_float(0x7fc00000u);
+    if (__builtin_isinf(x)) return y > 0.0f ? x : 0.0f;
+    return exp_(y * log_(x));
+}
+
+// float -> int32 with x86 cvttss2si semantics (used where the reference truncates to uchar)
+PT_DEV int32_t f2i_x86(float f)
+{
+    if (!(f > -2147483904.0f && f < 2147483648.0f)) return INT32_MIN;
+    return (int32_t)f;
+}
+
+// ---------------------------------------------------------------------------------------------
+// cuRAND XORWOW: d + v[5] kept in registers for a whole launch
+// ---------------------------------------------------------------------------------------------
+struct Xorwow { uint32_t d, v0, v1, v2, v3, v4; };
+
+PT_DEV Xorwow xorwow_init(uint64_t seed)
+{
+    const uint32_t s0 = (uint32_t)seed ^ 0xaad26b49u;
+    const uint32_t s1 = (uint32_t)(seed >> 32) ^ 0xf7dcefddu;
+    const uint32_t t0 = 1099087573u * s0;
+    const uint32_t t1 = 2591861531u * s1;
+    Xorwow s;
+    s.d = 6615241u + t1 + t0;
+    s.v0 = 123456789u + t0;
+    s.v1 = 362436069u ^ t0;
+    s.v2 = 521288629u + t1;
+    s.v3 = 88675123u ^ t1;
+    s.v4 = 5783321u + t0;
+    return s;
+}
+
+PT_DEV uint32_t xorwow_next(Xorwow& s)
+{
+    const uint32_t t = s.v0 ^ (s.v0 >> 2);
+    s.v0 = s.v1;
+    s.v1 = s.v2;
+    s.v2 = s.v3;
+    s.v3 = s.v4;
+    s.v4 = (s.v4 ^ (s.v4 << 4)) ^ (t ^ (t << 1));
+    s.d += 362437u;
+    return s.v4 + s.d;
+}
+
+PT_DEV float uniform(Xorwow& s)   // curand_uniform: (0, 1]
+{
+    return (float)xorwow_next(s) * 2.3283064e-10f + (2.3283064e-10f / 2.0f);
+}
+
+} // namespace pt
