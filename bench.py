@@ -44,7 +44,7 @@ def parse_args():
     p.add_argument("--chunk", type=int, default=8)
     p.add_argument("--cpu-baseline", type=int, default=1, help="time the oracle on a bounded sample (rank 0, N=1)")
     p.add_argument("--cpu-threads", type=int, default=0)
-    p.add_argument("--cpu-spp", type=int, default=32)
+    p.add_argument("--cpu-spp", type=int, default=192)
     return p.parse_args()
 
 
@@ -69,7 +69,7 @@ def cpu_baseline(args, W, H):
     """Oracle (plain-C restatement, pthreads) on a bounded sample of the same workload."""
     from oracle import pyoracle as po
     threads = args.cpu_threads or min(16, len(os.sched_getaffinity(0)))
-    stride = 4                     # every 4th row of the 1080p image
+    stride = 1                     # the full 1080p frame, fewer samples per pixel (~10 s of CPU work)
     sc = po.load_scene(args.scene, W, H)
     r = po.OracleRenderer(sc, W, H, 0, stride, threads=threads)
     spp = min(args.chunk, args.cpu_spp)
@@ -79,7 +79,7 @@ def cpu_baseline(args, W, H):
     dt = time.perf_counter() - t0
     samples = r.rows * W * spp * chunks
     return {"value": round(samples / dt / 1e6, 3), "unit": "Msamples/s", "cores": threads, "kind": "port",
-            "sample": f"{W}x{H} every {stride}th row ({r.rows} rows) x {spp * chunks} spp = {samples} samples, "
+            "sample": f"{W}x{H} rows 0::{stride} ({r.rows} rows) x {spp * chunks} spp = {samples} samples, "
                       f"{dt:.1f} s on {threads} threads"}
 
 

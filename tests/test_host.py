@@ -1,0 +1,176 @@
+"""Host C++ layer (libpt_host.so) without a GPU: scene loading, transforms, SAH BVH, camera and
+image I/O, checked against the independent oracle restatement and the reference's semantics."""
+import ctypes as C
+import json
+
+import numpy as np
+import pytest
+
+import pathtracercuda_amd as pa
+from oracle import pyoracle as po
+
+SCENES = ["cornell_box", "generated_scene", "test_shapes"]
+
+
+@pytest.mark.parametrize("name,W,H", [("cornell_box", 512, 512), ("generated_scene", 1920, 1080),
+                                      ("test_shapes", 320, 200), ("generated_scene", 3840, 2160)])
+def test_scene_and_bvh_match_oracle(scenes, name, W, H):
+    path = scenes / f"{name}.scene.json"
+    s = pa.Scene(path, W, H)
+    o = po.load_scene(path, W, H)
+    assert s.object_count == o.prim_count and s.node_count == o.node_count and s.skybox == o.skybox
+    nodes, prims = s.bvh()
+    assert bytes(nodes)[: 32 * s.node_count] == bytes(o.nodes)[: 32 * o.node_count]
+    assert bytes(prims) == bytes(o.prims)
+    assert bytes(s.camera()) == bytes(o.camera)
+    _, aabbs = s.objects()
+    oa = np.array([[*h.aabbMin, *h.aabbMax] for h in o.cpu], dtype=np.float32)
+    assert np.array_equal(aabbs.view(np.uint32), oa.view(np.uint32))
+    for a, b in zip(s.textures(), o.textures):
+        assert np.array_equal(a, b)
+
+
+def check_bvh_invariants(nodes, n_nodes, n_prims, maxleaf=4):
+    """BVH.cpp:36-52 validate() + layout: depth-first, left = i + 1, right = offset > i."""
+    reached = np.zeros(n_prims, dtype=int)
+    stack = [(0, 1)]
+    depth = 0
+    while stack:
+        i, d = stack.pop()
+        depth = max(depth, d)
+        nd = nodes[i]
+        cnt = nd.primitive_count_axis >> 16
+        if cnt:
+            assert 1 <= cnt <= maxleaf
+            reached[nd.offset:nd.offset + cnt] += 1
+        else:
+            axis = (nd.primitive_count_axis >> 8) & 0xFF
+            assert axis <= 2 and nd.offset > i + 1 and nd.offset < n_nodes
+            for c in (i + 1, nd.offset):
+                ch = nodes[c]
+                assert all(ch.aabb_min[k] >= nd.aabb_min[k] and ch.aabb_max[k] <= nd.aabb_max[k] for k in range(3))
+                stack.append((c, d + 1))
+    assert (reached == 1).all()
+    return depth
+
+
+@pytest.mark.parametrize("name", SCENES)
+def test_bvh_invariants(scenes, name):
+    s = pa.Scene(scenes / f"{name}.scene.json", 256, 256)
+    nodes, _ = s.bvh()
+    depth = check_bvh_invariants(nodes, s.node_count, s.object_count)
+    assert depth == s.bvh_depth and depth - 1 <= 32          # trace.cu:39 stack never overflows
+
+
+def test_bvh_degenerate_median_fallback(tmp_path):
+    # identical centroids defeat every SAH split -> std::nth_element fallback (BVH.cpp:190-207)
+    objs = [{"type": "SPHERE", "position": [0.0, 0.0, 0.0], "scale": [1.0 + 0.1 * i, 1.0, 1.0]} for i in range(37)]
+    objs += [{"type": "CUBE", "position": [float(i % 3), 0.0, 0.0]} for i in range(20)]
+    p = tmp_path / "degenerate.json"
+    p.write_text(json.dumps({"objects": objs}))
+    s = pa.Scene(p, 64, 64)
+    o = po.load_scene(p, 64, 64)
+    nodes, prims = s.bvh()
+    assert bytes(nodes)[: 32 * s.node_count] == bytes(o.nodes)[: 32 * o.node_count]
+    assert bytes(prims) == bytes(o.prims)
+    check_bvh_invariants(nodes, s.node_count, s.object_count)
+
+
+def test_bvh_random_scenes_match_oracle(tmp_path):
+    rng = np.random.default_rng(7)
+    for trial in range(4):
+        n = int(rng.integers(1, 400))
+        objs = []
+        for _ in range(n):
+            objs.append({"type": pa.HITTABLE_TYPES[int(rng.integers(0, 7))],
+                         "position": [float(x) for x in rng.normal(0, 4, 3)],
+                         "rotation": [float(x) for x in rng.uniform(-180, 180, 3)],
+                         "scale": [float(x) for x in rng.uniform(0.05, 2, 3)]})
+        p = tmp_path / f"rand{trial}.json"
+        p.write_text(json.dumps({"objects": objs}))
+        s = pa.Scene(p, 100, 50)
+        o = po.load_scene(p, 100, 50)
+        nodes, prims = s.bvh()
+        assert bytes(nodes)[: 32 * s.node_count] == bytes(o.nodes)[: 32 * o.node_count]
+        assert bytes(prims) == bytes(o.prims)
+
+
+def test_json_quirks(tmp_path, capfd):
+    scene = {"camera": {"position": [0, 1, 4], "look_at": [0, 1, 0], "fovy": 40},   # int fovy ignored -> 60
+             "objects": [
+                 {"type": "SPHERE", "material": {"type": "GGX", "roughness": 1, "metalness": 1}},  # ints ignored
+                 {"type": "TORUS", "material": {"type": "PLASTIC", "roughness": 0.01}},           # unknown strings
+             ]}
+    p = tmp_path / "q.json"
+    p.write_text(json.dumps(scene))
+    s = pa.Scene(p, 100, 100)
+    objs, _ = s.objects()
+    assert objs[0].material_type == 1 and abs(objs[0].roughness - 0.5) < 1e-7 and objs[0].metalness == 0.0
+    assert objs[1].type == 0 and objs[1].material_type == 0 and abs(objs[1].roughness - 0.04) < 1e-7  # clamp
+    out = capfd.readouterr().out
+    assert "Failed to parse object type: TORUS" in out and "Failed to parse material type: PLASTIC" in out
+    cam = s.camera()
+    ref = pa.make_camera((0, 1, 4), (0, 1, 0), fovy_radians=pa.radians(60.0), aspect=1.0)
+    assert bytes(cam) == bytes(ref)
+
+
+def test_scene_errors(tmp_path):
+    with pytest.raises(pa.PathtracerError, match="Failed to open"):
+        pa.Scene(tmp_path / "missing.json", 8, 8)
+    bad = tmp_path / "bad.json"
+    bad.write_text('{"objects": [ {"type": "SPHERE",, } ]}')
+    with pytest.raises(pa.PathtracerError, match="parse_error"):
+        pa.Scene(bad, 8, 8)
+    empty = tmp_path / "empty.json"
+    empty.write_text("{}")
+    s = pa.Scene(empty, 8, 8)
+    assert s.object_count == 0 and s.node_count == 0
+
+
+def test_missing_textures_get_handle_zero(tmp_path, scenes):
+    # earth.png is absent (Pathtracer.cpp:251-257 -> handle 0); the skybox then takes handle 1
+    s = pa.Scene(scenes / "generated_scene.scene.json", 64, 64)
+    assert s.skybox == 1 and len(s.textures()) == 1
+    objs, _ = s.objects()
+    assert all(o.texture_index == 0 for o in objs)
+
+
+def test_rgbe_reader_matches_python(scenes):
+    from oracle.pyoracle import read_rgbe
+    s = pa.Scene(scenes / "generated_scene.scene.json", 64, 64)
+    (sky,) = s.textures()
+    assert np.array_equal(sky, read_rgbe(scenes / "skybox.hdr"))
+    assert sky.shape == (256, 512, 4) and (sky[..., 3] == 1).all() and sky.max() > 10
+
+
+def test_png_reader_matches_pil(scenes):
+    from PIL import Image
+    s = pa.Scene(scenes / "test_shapes.scene.json", 64, 64)
+    tex = s.textures()
+    checker = tex[0]
+    ref = np.asarray(Image.open(scenes / "checker.png").convert("RGBA"), dtype=np.float32) / np.float32(255.0)
+    assert np.array_equal(checker, ref.astype(np.float32))
+
+
+def test_png_and_hdr_writers(tmp_path):
+    from PIL import Image
+    rng = np.random.default_rng(0)
+    img = rng.integers(0, 256, (13, 17, 4), dtype=np.uint8)
+    pa.write_png(str(tmp_path / "a.png"), img, flip=True)
+    back = np.asarray(Image.open(tmp_path / "a.png").convert("RGBA"))
+    assert np.array_equal(back, img[::-1])
+    hdr = rng.uniform(0, 50, (9, 11, 4)).astype(np.float32)
+    pa.write_hdr(str(tmp_path / "a.hdr"), hdr, flip=False)
+    back = po.read_rgbe(tmp_path / "a.hdr")
+    # RGBE shares one exponent: error <= max component / 128 (stbiw__linear_to_rgbe truncation)
+    tol = hdr[..., :3].max(-1, keepdims=True) / 128.0
+    assert (np.abs(back[..., :3] - hdr[..., :3]) <= tol).all()
+
+
+def test_camera_matches_oracle():
+    L = po.lib()
+    for pos, look, fovy, aspect in [((13, 2, 3), (0, 0, 0), 60.0, 16 / 9), ((0, 1, 4), (0, 1, 0), 40.0, 1.0)]:
+        c = pa.make_camera(pos, look, fovy_radians=pa.radians(fovy), aspect=float(np.float32(aspect)))
+        o = po.Camera()
+        L.or_camera_make(po.f3(pos), po.f3(look), po.f3([0, 1, 0]), L.or_radians(fovy), float(np.float32(aspect)), C.byref(o))
+        assert bytes(c) == bytes(o)
