@@ -140,6 +140,10 @@ PT_API int pt_read_rng(pt_context *ctx, uint32_t *dst);
 PT_API int pt_write_rng(pt_context *ctx, const uint32_t *src);
 
 PT_API uint32_t pt_local_rows(const pt_context *ctx);
+
+/* Tuning knob for A/B measurements: 0 = automatic (default); 1..5 select a trace-kernel variant
+ * (workgroup size, scene staged in LDS or read through the caches).  Results are identical. */
+PT_API int pt_set_kernel_variant(pt_context *ctx, int variant);
 PT_API const char *pt_last_error(const pt_context *ctx);
 
 #ifdef __cplusplus

@@ -208,6 +208,9 @@ class Pathtracer:
         d["ms"] = float(ms.value)
         return d
 
+    def set_kernel_variant(self, variant: int) -> None:
+        N.check_ctx(N.hip().pt_set_kernel_variant(self._ctx, int(variant)), self._ctx)
+
     def copy_accum_to_device(self, dst_ptr: int, nbytes: int) -> None:
         N.check_ctx(N.hip().pt_copy_accum_device(self._ctx, C.c_void_p(int(dst_ptr)), int(nbytes)), self._ctx)
 

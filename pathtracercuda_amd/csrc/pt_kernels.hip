@@ -56,6 +56,7 @@ struct TraceParams {
     uint32_t width, height, rowOffset, rowStride, rows;
     uint32_t spp, chunks, ignoreFirst;
     uint32_t tilesX, tilesY;
+    uint32_t nodeCount, primCount, stackDepth;
     DevCamera cam;
 };
 
@@ -196,9 +197,11 @@ struct Counters {
 
 // hitBVH (trace.cu:28-98): identical visit order, node culling with the current t_max, and
 // in-order leaf tests (later equal-t primitives win).  Returns the closest primitive or ~0u.
+// `stack` points at this lane's column of the wave's LDS stack ([depth][64 lanes] u32: entry k of
+// lane l is stack[64 * k], so one wave-wide push/pop touches 64 distinct banks-pairs, conflict-free).
 template <bool STATS>
-PT_DEV uint32_t traverse(const float4* __restrict__ nodes, const float4* __restrict__ prims, f3 o, f3 d, float& tHit,
-                         Counters& cnt)
+PT_DEV uint32_t traverse(const float4* __restrict__ nodes, const float4* __restrict__ prims, uint32_t* stack, f3 o,
+                         f3 d, float& tHit, Counters& cnt)
 {
     const float tMin = 0.001f;
     float tMax = kFltMax;
@@ -206,7 +209,6 @@ PT_DEV uint32_t traverse(const float4* __restrict__ nodes, const float4* __restr
     const float ix = 1.0f / d.x, iy = 1.0f / d.y, iz = 1.0f / d.z;
     // trace.cu:31-36: dirIsNeg from 1/(d != 0 ? d : 1e-7) < 0, i.e. d < 0
     const bool nx = d.x < 0.0f, ny = d.y < 0.0f, nz = d.z < 0.0f;
-    uint32_t stack[32];
     uint32_t sp = 0, cur = 0, elem = 0xffffffffu;
     for (;;) {
         const float4 A = nodes[2 * cur];
@@ -247,16 +249,16 @@ PT_DEV uint32_t traverse(const float4* __restrict__ nodes, const float4* __restr
                     }
                 }
                 if (sp == 0) break;
-                cur = stack[--sp];
+                cur = stack[64u * (--sp)];
             } else {
                 const uint32_t axis = (pca >> 8) & 0xffu;
                 const bool isNeg = axis == 0 ? nx : (axis == 1 ? ny : nz);
-                stack[sp++] = isNeg ? (cur + 1) : offset;
+                stack[64u * (sp++)] = isNeg ? (cur + 1) : offset;
                 cur = isNeg ? offset : (cur + 1);
             }
         } else {
             if (sp == 0) break;
-            cur = stack[--sp];
+            cur = stack[64u * (--sp)];
         }
     }
     tHit = tMax;
@@ -398,11 +400,24 @@ PT_DEV f3 specular_ggx(f3 F0, float NdotV, float NdotL, float NdotH, float VdotH
     return scale(D * Vis, F);
 }
 
-template <bool STATS>
-__global__ void __launch_bounds__(256) trace_kernel(TraceParams P)
+// LDS layout per workgroup: [scene nodes (2 float4 each) | scene prims (4 float4 each)] when
+// SCENE_LDS, then WPB wave stacks of stackDepth x 64 u32.
+template <bool STATS, bool SCENE_LDS, int WPB>
+__global__ void __launch_bounds__(WPB * 64) trace_kernel(TraceParams P)
 {
+    extern __shared__ float4 lds4[];
     const uint32_t lane = threadIdx.x & 63u;
-    const uint32_t tile = blockIdx.x * 4u + (threadIdx.x >> 6);
+    const uint32_t wave = threadIdx.x >> 6;
+    const uint32_t tile = blockIdx.x * (uint32_t)WPB + wave;
+    const uint32_t sceneF4 = SCENE_LDS ? 2u * P.nodeCount + 4u * P.primCount : 0u;
+    if (SCENE_LDS) {
+        for (uint32_t i = threadIdx.x; i < 2u * P.nodeCount; i += WPB * 64) lds4[i] = P.nodes[i];
+        for (uint32_t i = threadIdx.x; i < 4u * P.primCount; i += WPB * 64) lds4[2u * P.nodeCount + i] = P.prims[i];
+        __syncthreads();
+    }
+    const float4* __restrict__ nodes = SCENE_LDS ? lds4 : P.nodes;
+    const float4* __restrict__ prims = SCENE_LDS ? lds4 + 2u * P.nodeCount : P.prims;
+    uint32_t* stack = reinterpret_cast<uint32_t*>(lds4 + sceneF4) + wave * P.stackDepth * 64u + lane;
     const uint32_t tileX = tile % P.tilesX, tileY = tile / P.tilesX;
     const uint32_t px = tileX * 8u + (lane & 7u);
     const uint32_t ly = tileY * 8u + (lane >> 3);
@@ -440,7 +455,7 @@ __global__ void __launch_bounds__(256) trace_kernel(TraceParams P)
         while (alive) {
             if (STATS) cnt.segments++;
             float t;
-            const uint32_t e = traverse<STATS>(P.nodes, P.prims, o, d, t, cnt);
+            const uint32_t e = traverse<STATS>(nodes, prims, stack, o, d, t, cnt);
             bool pathEnd;
             if (e == 0xffffffffu) {                                       // trace.cu:115-134
                 f3 sky = splat(0.0f);
@@ -469,7 +484,7 @@ __global__ void __launch_bounds__(256) trace_kernel(TraceParams P)
                     const float4 m2 = P.mats[3 * e + 2];
                     const uint32_t texIdx = __float_as_uint(m2.x);
                     const uint32_t mtype = __float_as_uint(m2.y);
-                    const Surface sf = surface_of(P.prims, e, o, d, t, texIdx != 0);
+                    const Surface sf = surface_of(prims, e, o, d, t, texIdx != 0);
                     f3 tg, bt;
                     tangent_frame(sf.n, tg, bt);
                     const f3 wo = neg(d);                                 // MonteCarlo.h:21
@@ -629,7 +644,8 @@ struct pt_context {
     float4* nodes = nullptr;
     float4* prims = nullptr;
     float4* mats = nullptr;
-    uint32_t nodeCount = 0, primCount = 0;
+    uint32_t nodeCount = 0, primCount = 0, stackDepth = 1;
+    int variant = 0;
     DevTex* texTable = nullptr;
     DevTex hostTex[PT_MAX_TEXTURES] = {};
     uint32_t skybox = 0;
@@ -664,6 +680,46 @@ static int fail(pt_context* ctx, int code, const char* msg)
 {
     if (ctx) ctx->err = msg;
     return code;
+}
+
+// Kernel variants (workgroup size, scene staged in LDS or read through the caches).
+template <bool STATS, bool SL, int WPB>
+static hipError_t launch_one(const TraceParams& P, hipStream_t stream)
+{
+    const size_t sceneBytes = SL ? (2 * (size_t)P.nodeCount + 4 * (size_t)P.primCount) * sizeof(float4) : 0;
+    const size_t lds = sceneBytes + (size_t)WPB * P.stackDepth * 64 * sizeof(uint32_t);
+    if (lds > 160 * 1024) return hipErrorInvalidValue;
+    static bool attrSet = false;
+    if (!attrSet) {
+        hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(&trace_kernel<STATS, SL, WPB>),
+                                           hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+        if (e != hipSuccess) return e;
+        attrSet = true;
+    }
+    const uint32_t tiles = P.tilesX * P.tilesY;
+    const unsigned blocks = (tiles + WPB - 1) / WPB;
+    trace_kernel<STATS, SL, WPB><<<blocks, WPB * 64, lds, stream>>>(P);
+    return hipGetLastError();
+}
+
+template <bool STATS>
+static hipError_t launch_variant(int v, const TraceParams& P, hipStream_t stream)
+{
+    switch (v) {
+    case 1: return launch_one<STATS, false, 4>(P, stream);
+    case 2: return launch_one<STATS, true, 4>(P, stream);
+    case 3: return launch_one<STATS, true, 8>(P, stream);
+    case 4: return launch_one<STATS, true, 16>(P, stream);
+    case 5: return launch_one<STATS, false, 16>(P, stream);
+    default: return launch_one<STATS, true, 8>(P, stream);
+    }
+}
+
+static int pick_variant(const pt_context* ctx)
+{
+    if (ctx->variant > 0) return ctx->variant;
+    const size_t sceneBytes = (2 * (size_t)ctx->nodeCount + 4 * (size_t)ctx->primCount) * sizeof(float4);
+    return sceneBytes <= 96 * 1024 ? 3 : 5;
 }
 
 extern "C" {
@@ -736,7 +792,8 @@ PT_API void pt_destroy(pt_context* ctx)
 
 // Host-side validation of the BVH so a malformed scene can never make the kernel read out of
 // bounds or overflow its 32-entry stack (the reference does not check, trace.cu:39).
-static int validate_scene(pt_context* ctx, const pt_bvh_node* nodes, uint32_t nn, const pt_hittable* prims, uint32_t np)
+static int validate_scene(pt_context* ctx, const pt_bvh_node* nodes, uint32_t nn, const pt_hittable* prims, uint32_t np,
+                          uint32_t& maxDepthOut)
 {
     for (uint32_t i = 0; i < np; ++i) {
         if (prims[i].type > 6u) return fail(ctx, PT_ERR_ARG, "pt_set_scene: invalid hittable type");
@@ -765,6 +822,7 @@ static int validate_scene(pt_context* ctx, const pt_bvh_node* nodes, uint32_t nn
         }
     }
     if (maxDepth > 33) return fail(ctx, PT_ERR_DEPTH, "pt_set_scene: BVH depth exceeds the 32-entry traversal stack");
+    maxDepthOut = maxDepth;
     return PT_OK;
 }
 
@@ -773,7 +831,8 @@ PT_API int pt_set_scene(pt_context* ctx, const pt_bvh_node* nodes, uint32_t node
 {
     if (!ctx) return PT_ERR_ARG;
     if (node_count == 0 || prim_count == 0 || !nodes || !prims) return fail(ctx, PT_ERR_ARG, "pt_set_scene: empty scene");
-    int rc = validate_scene(ctx, nodes, node_count, prims, prim_count);
+    uint32_t maxDepth = 1;
+    int rc = validate_scene(ctx, nodes, node_count, prims, prim_count, maxDepth);
     if (rc != PT_OK) return rc;
     std::vector<float4> hn(2 * (size_t)node_count), hp(4 * (size_t)prim_count), hm(3 * (size_t)prim_count);
     for (uint32_t i = 0; i < node_count; ++i) {
@@ -807,6 +866,8 @@ PT_API int pt_set_scene(pt_context* ctx, const pt_bvh_node* nodes, uint32_t node
     PT_HIP_CHECK(ctx, hipMemcpy(ctx->mats, hm.data(), hm.size() * sizeof(float4), hipMemcpyHostToDevice));
     ctx->nodeCount = node_count;
     ctx->primCount = prim_count;
+    // a traversal holds at most one pending sibling per interior ancestor: depth - 1 entries
+    ctx->stackDepth = maxDepth > 1 ? maxDepth - 1 : 1;
     return PT_OK;
 }
 
@@ -874,12 +935,13 @@ static int render_impl(pt_context* ctx, const pt_camera* cam, uint32_t spp, uint
     P.cam.llc = hf3(cam->lower_left_corner);
     P.cam.horizontal = hf3(cam->horizontal);
     P.cam.vertical = hf3(cam->vertical);
-    const uint32_t tiles = P.tilesX * P.tilesY;
-    const unsigned blocks = (tiles + 3) / 4;
+    P.nodeCount = ctx->nodeCount;
+    P.primCount = ctx->primCount;
+    P.stackDepth = ctx->stackDepth;
     if (stats) PT_HIP_CHECK(ctx, hipMemsetAsync(ctx->stats, 0, 8 * sizeof(unsigned long long), ctx->stream));
     PT_HIP_CHECK(ctx, hipEventRecord(ctx->ev0, ctx->stream));
-    if (stats) trace_kernel<true><<<blocks, 256, 0, ctx->stream>>>(P);
-    else trace_kernel<false><<<blocks, 256, 0, ctx->stream>>>(P);
+    const int variant = pick_variant(ctx);
+    PT_HIP_CHECK(ctx, stats ? launch_variant<true>(variant, P, ctx->stream) : launch_variant<false>(variant, P, ctx->stream));
     PT_HIP_CHECK(ctx, hipGetLastError());
     PT_HIP_CHECK(ctx, hipEventRecord(ctx->ev1, ctx->stream));
     PT_HIP_CHECK(ctx, hipEventSynchronize(ctx->ev1));
@@ -976,6 +1038,13 @@ PT_API int pt_write_rng(pt_context* ctx, const uint32_t* src)
 }
 
 PT_API uint32_t pt_local_rows(const pt_context* ctx) { return ctx ? ctx->rows : 0; }
+
+PT_API int pt_set_kernel_variant(pt_context* ctx, int variant)
+{
+    if (!ctx || variant < 0 || variant > 5) return PT_ERR_ARG;
+    ctx->variant = variant;
+    return PT_OK;
+}
 
 PT_API const char* pt_last_error(const pt_context* ctx) { return ctx ? ctx->err.c_str() : "null context"; }
 

@@ -1,0 +1,57 @@
+"""A/B timing of the trace-kernel variants in one process (interleaved rounds), with a bit-exact
+cross-check of every variant's accumulation against variant 1.  Usage on the GPU box:
+    python tools/ab_variants.py [--spp 64] [--rounds 5] [--variants 1,2,3,4,5] [--scene ...]
+"""
+import argparse
+import json
+import pathlib
+import sys
+import time
+
+import numpy as np
+
+ROOT = pathlib.Path(__file__).resolve().parents[1]
+sys.path.insert(0, str(ROOT))
+import pathtracercuda_amd as pa  # noqa: E402
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--scene", default=str(ROOT / "scenes/generated_scene.scene.json"))
+    ap.add_argument("--width", type=int, default=1920)
+    ap.add_argument("--height", type=int, default=1080)
+    ap.add_argument("--spp", type=int, default=64)
+    ap.add_argument("--rounds", type=int, default=5)
+    ap.add_argument("--variants", default="1,2,3,4,5")
+    a = ap.parse_args()
+    vs = [int(v) for v in a.variants.split(",")]
+    pt = pa.Pathtracer(a.width, a.height)
+    cam = pt.load_scene(a.scene)
+    chunks = a.spp // 8
+    ref = None
+    times = {v: [] for v in vs}
+    for v in vs:                                   # correctness first: every variant bit-identical
+        pt.set_kernel_variant(v)
+        st = pt.rng_state()
+        pt.render_raw(cam, 8, 1, True)
+        acc = pt.accum()
+        pt.set_rng_state(st)
+        if ref is None:
+            ref = acc
+        assert np.array_equal(acc.view(np.uint32), ref.view(np.uint32)), f"variant {v} differs"
+    for r in range(a.rounds):
+        for v in vs:
+            pt.set_kernel_variant(v)
+            ms = pt.render_raw(cam, 8, chunks, True)
+            times[v].append(ms)
+    samples = a.width * a.height * a.spp
+    out = {}
+    for v in vs:
+        t = np.array(times[v])
+        out[v] = {"median_ms": float(np.median(t)), "min_ms": float(t.min()),
+                  "Msamples_s": round(samples / (np.median(t) / 1e3) / 1e6, 1)}
+    print(json.dumps({"scene": pathlib.Path(a.scene).name, "spp": a.spp, "variants": out}))
+
+
+if __name__ == "__main__":
+    main()
