@@ -80,6 +80,13 @@ typedef struct pt_render_stats {
     uint64_t sky_lookups;  /* misses that sampled the skybox texture  */
     uint64_t segments;     /* hitBVH calls                            */
     uint64_t samples;      /* camera paths                            */
+    /* wave-level executions of the same events: SIMD efficiency of a phase = lane count / (64 x
+     * wave count) */
+    uint64_t wave_node_iters;
+    uint64_t wave_prim_iters;
+    uint64_t wave_hits;
+    uint64_t wave_sky;
+    uint64_t wave_segments;
 } pt_render_stats;
 
 typedef struct pt_context pt_context;

@@ -39,7 +39,9 @@ class PtHittable(C.Structure):
 
 class PtRenderStats(C.Structure):
     _fields_ = [("node_tests", C.c_uint64), ("prim_tests", C.c_uint64), ("hits", C.c_uint64),
-                ("sky_lookups", C.c_uint64), ("segments", C.c_uint64), ("samples", C.c_uint64)]
+                ("sky_lookups", C.c_uint64), ("segments", C.c_uint64), ("samples", C.c_uint64),
+                ("wave_node_iters", C.c_uint64), ("wave_prim_iters", C.c_uint64), ("wave_hits", C.c_uint64),
+                ("wave_sky", C.c_uint64), ("wave_segments", C.c_uint64)]
 
 
 # symbol -> (restype, argtypes); the CPU test suite checks that every declaration in include/*.h

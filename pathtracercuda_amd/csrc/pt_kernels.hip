@@ -56,7 +56,7 @@ struct TraceParams {
     uint32_t width, height, rowOffset, rowStride, rows;
     uint32_t spp, chunks, ignoreFirst;
     uint32_t tilesX, tilesY;
-    uint32_t nodeCount, primCount, stackDepth;
+    uint32_t nodeCount, primCount, stackDepth, slabFast;
     DevCamera cam;
 };
 
@@ -99,15 +99,30 @@ enum : uint32_t { SPHERE = 0, CYLINDER = 1, DISK = 2, CONE = 3, PARABOLOID = 4, 
 
 struct LocalRay { f3 o, d; };
 
-// Hittable.inl:91-98: world -> object space with the 3x4 inverse rows (origin gets +w)
-PT_DEV LocalRay to_local(const float4& r0, const float4& r1, const float4& r2, f3 o, f3 d)
+typedef float f2v __attribute__((ext_vector_type(2)));   // lowers to v_pk_{add,mul}_f32 on gfx950
+
+PT_DEV f2v f2(float a, float b) { return (f2v){a, b}; }
+
+// Hittable.inl:91-98: world -> object space with the 3x4 inverse rows (origin gets +w).  Device
+// layout of the rows (pt_set_scene): P0 = (r0.x, r1.x, r0.y, r1.y), P1 = (r0.z, r1.z, r0.w, r1.w),
+// P2 = row 2, so the x and y components are evaluated pairwise with packed FP32 ops -- the same
+// products and sums in the same order as the reference's dot products, two lanes of a
+// v_pk_mul/v_pk_add at a time (exactly rounded per element; no FMA contraction).
+PT_DEV LocalRay to_local(const float4& P0, const float4& P1, const float4& r2, f3 o, f3 d)
 {
     LocalRay l;
-    l.o.x = (o.x * r0.x + o.y * r0.y + o.z * r0.z) + r0.w;
-    l.o.y = (o.x * r1.x + o.y * r1.y + o.z * r1.z) + r1.w;
+    f2v oxy = f2(P0.x, P0.y) * f2(o.x, o.x);
+    oxy = oxy + f2(P0.z, P0.w) * f2(o.y, o.y);
+    oxy = oxy + f2(P1.x, P1.y) * f2(o.z, o.z);
+    oxy = oxy + f2(P1.z, P1.w);
+    f2v dxy = f2(P0.x, P0.y) * f2(d.x, d.x);
+    dxy = dxy + f2(P0.z, P0.w) * f2(d.y, d.y);
+    dxy = dxy + f2(P1.x, P1.y) * f2(d.z, d.z);
+    l.o.x = oxy.x;
+    l.o.y = oxy.y;
     l.o.z = (o.x * r2.x + o.y * r2.y + o.z * r2.z) + r2.w;
-    l.d.x = d.x * r0.x + d.y * r0.y + d.z * r0.z;
-    l.d.y = d.x * r1.x + d.y * r1.y + d.z * r1.z;
+    l.d.x = dxy.x;
+    l.d.y = dxy.y;
     l.d.z = d.x * r2.x + d.y * r2.y + d.z * r2.z;
     return l;
 }
@@ -193,72 +208,170 @@ PT_DEV bool prim_hit(const float4* __restrict__ prims, uint32_t p, f3 o, f3 d, f
 
 struct Counters {
     uint32_t node_tests, prim_tests, hits, sky, segments, samples;
+    // wave-level executions of the same points (SIMD efficiency = lane count / (64 * wave count))
+    uint32_t w_node, w_prim, w_hits, w_sky, w_segments;
 };
+
+// Counts one per wave that executes this point (instrumented variant only).
+PT_DEV void wave_tick(uint32_t& c)
+{
+    const unsigned long long m = __ballot(1);
+    if ((threadIdx.x & 63u) == (uint32_t)(__ffsll((long long)m) - 1)) c++;
+}
 
 // hitBVH (trace.cu:28-98): identical visit order, node culling with the current t_max, and
 // in-order leaf tests (later equal-t primitives win).  Returns the closest primitive or ~0u.
 // `stack` points at this lane's column of the wave's LDS stack ([depth][64 lanes] u32: entry k of
 // lane l is stack[64 * k], so one wave-wide push/pop touches 64 distinct banks-pairs, conflict-free).
-template <bool STATS>
+// Slab test of node `cur` against the ray's running interval (AABB.inl:22-44).  The reference
+// recomputes 1/d per node and axis, a function of the ray only, so it is hoisted (bit-identical);
+// the early returns are dropped because both bounds are monotone and never NaN.  Device node
+// layout (pt_set_scene): A = (min.x, max.x, min.y, max.y), B = (min.z, max.z, offset, pca).
+struct NodeHit {
+    bool hit;
+    uint32_t offset, pca;
+};
+
+// Exact form for any ray: swap on negative 1/d, NaN products ignored by the selects.
+PT_DEV NodeHit node_test(const float4* __restrict__ nodes, uint32_t cur, f3 o, float ix, float iy, float iz, float tMin,
+                         float tMax)
+{
+    const float4 A = nodes[2 * cur];
+    const float4 Bq = nodes[2 * cur + 1];
+    float lo = tMin, hi = tMax;
+    {
+        float t0 = (A.x - o.x) * ix, t1 = (A.y - o.x) * ix;
+        if (ix < 0.0f) { const float tmp = t0; t0 = t1; t1 = tmp; }
+        lo = t0 > lo ? t0 : lo;
+        hi = t1 < hi ? t1 : hi;
+    }
+    {
+        float t0 = (A.z - o.y) * iy, t1 = (A.w - o.y) * iy;
+        if (iy < 0.0f) { const float tmp = t0; t0 = t1; t1 = tmp; }
+        lo = t0 > lo ? t0 : lo;
+        hi = t1 < hi ? t1 : hi;
+    }
+    {
+        float t0 = (Bq.x - o.z) * iz, t1 = (Bq.y - o.z) * iz;
+        if (iz < 0.0f) { const float tmp = t0; t0 = t1; t1 = tmp; }
+        lo = t0 > lo ? t0 : lo;
+        hi = t1 < hi ? t1 : hi;
+    }
+    return NodeHit{hi > lo, __float_as_uint(Bq.z), __float_as_uint(Bq.w)};
+}
+
+// Fast form, exact when 1/d is finite on all axes and the box is not inverted (checked per ray
+// and per scene): then no product is NaN, the swap on a negative 1/d is min/max of the two slab
+// distances, and the running max/min over the axes is order-independent, so v_max3/v_min3 and
+// packed subtract/multiply give the reference's values.
+PT_DEV NodeHit node_test_fast(const float4* __restrict__ nodes, uint32_t cur, f2v ox2, f2v oy2, f2v oz2, f2v ix2,
+                              f2v iy2, f2v iz2, float tMin, float tMax)
+{
+    const float4 A = nodes[2 * cur];
+    const float4 Bq = nodes[2 * cur + 1];
+    const f2v tx = (f2(A.x, A.y) - ox2) * ix2;
+    const f2v ty = (f2(A.z, A.w) - oy2) * iy2;
+    const f2v tz = (f2(Bq.x, Bq.y) - oz2) * iz2;
+    const float lo = __builtin_fmaxf(__builtin_fmaxf(tMin, __builtin_fminf(tx.x, tx.y)),
+                                     __builtin_fmaxf(__builtin_fminf(ty.x, ty.y), __builtin_fminf(tz.x, tz.y)));
+    const float hi = __builtin_fminf(__builtin_fminf(tMax, __builtin_fmaxf(tx.x, tx.y)),
+                                     __builtin_fminf(__builtin_fmaxf(ty.x, ty.y), __builtin_fmaxf(tz.x, tz.y)));
+    return NodeHit{hi > lo, __float_as_uint(Bq.z), __float_as_uint(Bq.w)};
+}
+
+// hitBVH (trace.cu:28-98): identical per-lane visit order, node culling with the current t_max,
+// and in-order leaf tests (later equal-t primitives win).  Returns the closest primitive or ~0u.
+// `stack` points at this lane's column of the wave's LDS stack ([depth][64 lanes] u32: entry k of
+// lane l is stack[64 * k], so a wave-wide push/pop is bank-conflict free).
+//
+// WW = false: one loop, a visited leaf is tested immediately (the reference's control flow).
+// WW = true ("while-while"): each lane walks interior nodes until it reaches a leaf to test (or
+// finishes); then the wave tests the pending leaves together.  The per-lane sequence of node and
+// primitive tests is unchanged -- only the SIMD schedule differs -- so results are bit-identical,
+// but the expensive primitive tests run with most lanes active instead of once per node step.
+template <bool STATS, bool WW>
 PT_DEV uint32_t traverse(const float4* __restrict__ nodes, const float4* __restrict__ prims, uint32_t* stack, f3 o,
-                         f3 d, float& tHit, Counters& cnt)
+                         f3 d, bool slabFast, float& tHit, Counters& cnt)
 {
     const float tMin = 0.001f;
     float tMax = kFltMax;
-    // AABB.inl:29 recomputes 1/d per node and axis; the value is a function of the ray only.
     const float ix = 1.0f / d.x, iy = 1.0f / d.y, iz = 1.0f / d.z;
     // trace.cu:31-36: dirIsNeg from 1/(d != 0 ? d : 1e-7) < 0, i.e. d < 0
-    const bool nx = d.x < 0.0f, ny = d.y < 0.0f, nz = d.z < 0.0f;
+    const uint32_t negMask = (d.x < 0.0f ? 1u : 0u) | (d.y < 0.0f ? 2u : 0u) | (d.z < 0.0f ? 4u : 0u);
+    const bool fast = slabFast && __builtin_isfinite(ix) && __builtin_isfinite(iy) && __builtin_isfinite(iz);
+    const f2v ox2 = f2(o.x, o.x), oy2 = f2(o.y, o.y), oz2 = f2(o.z, o.z);
+    const f2v ix2 = f2(ix, ix), iy2 = f2(iy, iy), iz2 = f2(iz, iz);
+    auto test = [&](uint32_t node) {
+        return fast ? node_test_fast(nodes, node, ox2, oy2, oz2, ix2, iy2, iz2, tMin, tMax)
+                    : node_test(nodes, node, o, ix, iy, iz, tMin, tMax);
+    };
     uint32_t sp = 0, cur = 0, elem = 0xffffffffu;
-    for (;;) {
-        const float4 A = nodes[2 * cur];
-        const float4 Bq = nodes[2 * cur + 1];
-        if (STATS) cnt.node_tests++;
-        // AABB.inl:22-44, swap-on-negative and the running [tMin, tMax] interval.  The early
-        // returns are dropped: both bounds are monotone and never NaN, so the final test is equal.
-        float lo = tMin, hi = tMax;
-        {
-            float t0 = (A.x - o.x) * ix, t1 = (A.w - o.x) * ix;
-            if (ix < 0.0f) { const float tmp = t0; t0 = t1; t1 = tmp; }
-            lo = t0 > lo ? t0 : lo;
-            hi = t1 < hi ? t1 : hi;
-        }
-        {
-            float t0 = (A.y - o.y) * iy, t1 = (Bq.x - o.y) * iy;
-            if (iy < 0.0f) { const float tmp = t0; t0 = t1; t1 = tmp; }
-            lo = t0 > lo ? t0 : lo;
-            hi = t1 < hi ? t1 : hi;
-        }
-        {
-            float t0 = (A.z - o.z) * iz, t1 = (Bq.y - o.z) * iz;
-            if (iz < 0.0f) { const float tmp = t0; t0 = t1; t1 = tmp; }
-            lo = t0 > lo ? t0 : lo;
-            hi = t1 < hi ? t1 : hi;
-        }
-        const uint32_t offset = __float_as_uint(Bq.z);
-        const uint32_t pca = __float_as_uint(Bq.w);
-        if (hi > lo) {
-            const uint32_t count = pca >> 16;
-            if (count > 0) {
-                for (uint32_t i = 0; i < count; ++i) {
-                    if (STATS) cnt.prim_tests++;
-                    float t;
-                    if (prim_hit(prims, offset + i, o, d, tMin, tMax, t)) {
-                        tMax = t;
-                        elem = offset + i;
+    if (!WW) {
+        for (;;) {
+            if (STATS) { cnt.node_tests++; wave_tick(cnt.w_node); }
+            const NodeHit nh = test(cur);
+            if (nh.hit) {
+                const uint32_t count = nh.pca >> 16;
+                if (count > 0) {
+                    for (uint32_t i = 0; i < count; ++i) {
+                        if (STATS) { cnt.prim_tests++; wave_tick(cnt.w_prim); }
+                        float t;
+                        if (prim_hit(prims, nh.offset + i, o, d, tMin, tMax, t)) {
+                            tMax = t;
+                            elem = nh.offset + i;
+                        }
                     }
+                    if (sp == 0) break;
+                    cur = stack[64u * (--sp)];
+                } else {
+                    const bool isNeg = (negMask >> ((nh.pca >> 8) & 0xffu)) & 1u;
+                    stack[64u * (sp++)] = isNeg ? (cur + 1) : nh.offset;
+                    cur = isNeg ? nh.offset : (cur + 1);
                 }
+            } else {
                 if (sp == 0) break;
                 cur = stack[64u * (--sp)];
-            } else {
-                const uint32_t axis = (pca >> 8) & 0xffu;
-                const bool isNeg = axis == 0 ? nx : (axis == 1 ? ny : nz);
-                stack[64u * (sp++)] = isNeg ? (cur + 1) : offset;
-                cur = isNeg ? offset : (cur + 1);
             }
-        } else {
-            if (sp == 0) break;
-            cur = stack[64u * (--sp)];
+        }
+    } else {
+        uint32_t leafOff = 0, leafCnt = 0;
+        bool done = false;
+        while (!done) {
+            while (leafCnt == 0 && !done) {                     // interior walk
+                if (STATS) { cnt.node_tests++; wave_tick(cnt.w_node); }
+                const NodeHit nh = test(cur);
+                const uint32_t count = nh.pca >> 16;
+                const bool isNeg = (negMask >> ((nh.pca >> 8) & 0xffu)) & 1u;
+                const uint32_t nearC = isNeg ? nh.offset : cur + 1;
+                const uint32_t farC = isNeg ? cur + 1 : nh.offset;
+                if (nh.hit) {
+                    if (count > 0) {
+                        leafOff = nh.offset;
+                        leafCnt = count;
+                    } else {
+                        stack[64u * sp] = farC;
+                        ++sp;
+                        cur = nearC;
+                    }
+                } else {
+                    if (sp == 0) done = true;
+                    else cur = stack[64u * (--sp)];
+                }
+            }
+            while (leafCnt > 0) {                                // pending leaf, in order
+                if (STATS) { cnt.prim_tests++; wave_tick(cnt.w_prim); }
+                float t;
+                if (prim_hit(prims, leafOff, o, d, tMin, tMax, t)) {
+                    tMax = t;
+                    elem = leafOff;
+                }
+                ++leafOff;
+                --leafCnt;
+            }
+            if (!done) {
+                if (sp == 0) done = true;
+                else cur = stack[64u * (--sp)];
+            }
         }
     }
     tHit = tMax;
@@ -323,9 +436,9 @@ PT_DEV Surface surface_of(const float4* __restrict__ prims, uint32_t e, f3 o, f3
     }
     }
     f3 tmp;                                                 // Hittable.inl:131-134
-    tmp.x = n.x * r0.x + n.y * r1.x + n.z * r2.x;
-    tmp.y = n.x * r0.y + n.y * r1.y + n.z * r2.y;
-    tmp.z = n.x * r0.z + n.y * r1.z + n.z * r2.z;
+    tmp.x = n.x * r0.x + n.y * r0.y + n.z * r2.x;           // (r0.x, r1.x, r2.x)
+    tmp.y = n.x * r0.z + n.y * r0.w + n.z * r2.y;           // (r0.y, r1.y, r2.y)
+    tmp.z = n.x * r1.x + n.y * r1.y + n.z * r2.z;           // (r0.z, r1.z, r2.z)
     Surface s;
     s.p = add(o, scale(t, d));
     const f3 on = normalize(tmp);
@@ -400,193 +513,349 @@ PT_DEV f3 specular_ggx(f3 F0, float NdotV, float NdotL, float NdotH, float VdotH
     return scale(D * Vis, F);
 }
 
+// Per-lane path state of the megakernel (trace.cu:158-199 + getColor's loop variables).
+struct PathState {
+    f3 o, d;          // current ray
+    f3 L, T;          // radiance and throughput of the current path (trace.cu:104-105)
+    f3 color;         // sum of the finished paths of the current render() call (trace.cu:186)
+    f3 accum;         // accumulation buffer value of this pixel
+    uint32_t s, c, bounce;
+    bool alive;
+};
+
+// camera ray of one sample (trace.cu:190-192, Camera.inl:25-28): two uniforms, x then y
+PT_DEV void camera_ray(const TraceParams& P, float fx, float fy, Xorwow& rng, f3& o, f3& d)
+{
+    const float u = (fx + uniform(rng)) / (float)P.width;
+    const float v = (fy + uniform(rng)) / (float)P.height;
+    o = P.cam.origin;
+    d = normalize(add(add(P.cam.llc, scale(u, P.cam.horizontal)), scale(v, P.cam.vertical)));
+}
+
+// One iteration of getColor's bounce loop after hitBVH (trace.cu:114-152): miss -> sky, hit ->
+// emission + Material::sample + throughput update.  Returns true when the path ends.
+template <bool STATS>
+PT_DEV bool shade(const TraceParams& P, const float4* __restrict__ prims, uint32_t e, float t, PathState& ps,
+                  Xorwow& rng, Counters& cnt)
+{
+    if (e == 0xffffffffu) {                                                   // trace.cu:115-134
+        f3 sky = splat(0.0f);
+        if (P.skybox != 0) {
+            if (STATS) { cnt.sky++; wave_tick(cnt.w_sky); }
+            const float theta = acos_(ps.d.y);
+            const float phi = atan2_(ps.d.z, ps.d.x);
+            const float v = theta / kPi;
+            const float u = phi / kTwoPi;
+            sky = tex2d(P.textures[P.skybox - 1], u, v);
+        }
+        ps.L = add(ps.L, mul(ps.T, sky));
+        return true;
+    }
+    if (STATS) { cnt.hits++; wave_tick(cnt.w_hits); }
+    const float4 m0 = P.mats[3 * e + 0];
+    const float4 m1 = P.mats[3 * e + 1];
+    ps.L = add(ps.L, mul(ps.T, mk(m1.x, m1.y, m1.z)));                      // trace.cu:139
+    if (ps.bounce == 4) {
+        // 5th segment: its scattered ray is discarded (trace.cu:109); only the two uniforms of
+        // Material.inl:40-41 are observable.
+        (void)uniform(rng);
+        (void)uniform(rng);
+        return true;
+    }
+    const float4 m2 = P.mats[3 * e + 2];
+    const uint32_t texIdx = __float_as_uint(m2.x);
+    const uint32_t mtype = __float_as_uint(m2.y);
+    const Surface sf = surface_of(prims, e, ps.o, ps.d, t, texIdx != 0);
+    f3 tg, bt;
+    tangent_frame(sf.n, tg, bt);
+    const f3 wo = neg(ps.d);                                                  // MonteCarlo.h:15-22
+    const f3 V = normalize(add(add(scale(wo.x, mk(tg.x, bt.x, sf.n.x)), scale(wo.y, mk(tg.y, bt.y, sf.n.y))),
+                               scale(wo.z, mk(tg.z, bt.z, sf.n.z))));
+    f3 base = mk(m0.x, m0.y, m0.z);
+    if (texIdx != 0) {                                                        // Material.inl:26-35
+        const f3 tap = tex2d(P.textures[texIdx - 1], sf.u, sf.v);
+        base = mk(pow_(tap.x, 2.2f), pow_(tap.y, 2.2f), pow_(tap.z, 2.2f));
+    }
+    float rnd0 = uniform(rng);
+    const float rnd1 = uniform(rng);
+    const float rough = m0.w, metal = m1.w;
+    const float a = rough * rough;
+    const float a2 = a * a;
+    f3 dir = splat(0.0f), att = splat(0.0f);
+    float pdf = 0.0f;
+    bool killed = false;
+    if (mtype == 0u) {                                                        // LAMBERT (Material.inl:67-72)
+        dir = cosine_sample(rnd0, rnd1);
+        pdf = dir.z / kPi;
+        att = scale(kInvPi, base);
+    } else if (mtype <= 2u) {
+        bool specular = true;
+        if (mtype == 2u) {                                                    // LAMBERT_GGX (:101-144)
+            if (rnd0 < 0.5f) { rnd0 = 2.0f * rnd0; specular = false; }
+            else rnd0 = 2.0f * (rnd0 - 0.5f);
+        }
+        if (specular) dir = reflect(neg(V), vndf_sample(V, rnd0, rnd1, a));
+        else dir = cosine_sample(rnd0, rnd1);
+        if (dir.z < 0.0f) {
+            killed = true;                                                    // pdf = 1, attenuation 0
+        } else {
+            const float NdotV = fabsf(V.z) + 1e-5f;
+            const f3 H = normalize(add(V, dir));
+            const float VdotH = clamp01(dot(V, H));
+            const float NdotH = clamp01(H.z);
+            const float NdotL = clamp01(dir.z);
+            const float ggxPdf = vndf_pdf(H, V, a);
+            const f3 F0 = lerp(splat(0.04f), base, metal);
+            const f3 kS = specular_ggx(F0, NdotV, NdotL, NdotH, VdotH, a2);
+            if (mtype == 1u) {                                                // GGX (:74-99)
+                pdf = ggxPdf;
+                att = kS;
+            } else {
+                const float cosinePdf = dir.z / kPi;
+                pdf = (ggxPdf + cosinePdf) * 0.5f;
+                att = add(scale(1.0f - metal, scale(kInvPi, base)), kS);
+            }
+        }
+    }
+    if (killed || is_zero(att) || pdf == 0.0f) return true;                  // trace.cu:145-148
+    // Material.inl:57: normalize(tangentToWorld(...)), which itself normalizes
+    const f3 sd = normalize(normalize(add(add(scale(dir.x, tg), scale(dir.y, bt)), scale(dir.z, sf.n))));
+    const f3 w = divs(scale(fabsf(dot(sd, sf.n)), att), pdf);                 // trace.cu:150
+    ps.T = mul(ps.T, w);
+    ps.o = sf.p;
+    ps.d = sd;
+    ++ps.bounce;
+    return false;
+}
+
+// End of a path: sum it into the render() call's color; at the end of a call fold the call into
+// the accumulation value (trace.cu:193-198); start the next sample while any remain.
+template <bool STATS>
+PT_DEV void finish_path(const TraceParams& P, PathState& ps, Xorwow& rng, float fx, float fy, Counters& cnt)
+{
+    ps.color = add(ps.color, ps.L);
+    if (STATS) cnt.samples++;
+    if (++ps.s == P.spp) {
+        const bool ignore = (ps.c == 0) && P.ignoreFirst;
+        ps.accum = ignore ? ps.color : add(ps.color, ps.accum);
+        ps.color = splat(0.0f);
+        ps.s = 0;
+        if (++ps.c == P.chunks) ps.alive = false;
+    }
+    if (ps.alive) {
+        camera_ray(P, fx, fy, rng, ps.o, ps.d);
+        ps.L = splat(0.0f);
+        ps.T = splat(1.0f);
+        ps.bounce = 0;
+    }
+}
+
+template <bool STATS>
+PT_DEV void flush_counters(const TraceParams& P, const Counters& cnt)
+{
+    if (!STATS) return;
+    atomicAdd(&P.stats[0], (unsigned long long)cnt.node_tests);
+    atomicAdd(&P.stats[1], (unsigned long long)cnt.prim_tests);
+    atomicAdd(&P.stats[2], (unsigned long long)cnt.hits);
+    atomicAdd(&P.stats[3], (unsigned long long)cnt.sky);
+    atomicAdd(&P.stats[4], (unsigned long long)cnt.segments);
+    atomicAdd(&P.stats[5], (unsigned long long)cnt.samples);
+    atomicAdd(&P.stats[6], (unsigned long long)cnt.w_node);
+    atomicAdd(&P.stats[7], (unsigned long long)cnt.w_prim);
+    atomicAdd(&P.stats[8], (unsigned long long)cnt.w_hits);
+    atomicAdd(&P.stats[9], (unsigned long long)cnt.w_sky);
+    atomicAdd(&P.stats[10], (unsigned long long)cnt.w_segments);
+}
+
+struct PixelCtx {
+    bool valid;
+    uint32_t px, py;
+    size_t li, npix;
+};
+
+PT_DEV PixelCtx pixel_of(const TraceParams& P, uint32_t tile, uint32_t lane)
+{
+    PixelCtx pc;
+    const uint32_t tileX = tile % P.tilesX, tileY = tile / P.tilesX;
+    pc.px = tileX * 8u + (lane & 7u);
+    const uint32_t ly = tileY * 8u + (lane >> 3);
+    pc.valid = tileY < P.tilesY && pc.px < P.width && ly < P.rows;
+    pc.py = P.rowOffset + ly * P.rowStride;
+    pc.npix = (size_t)P.rows * P.width;
+    pc.li = (size_t)ly * P.width + pc.px;
+    return pc;
+}
+
+PT_DEV void load_pixel(const TraceParams& P, const PixelCtx& pc, Xorwow& rng, PathState& ps)
+{
+    rng.d = P.rng[pc.li];
+    rng.v0 = P.rng[pc.npix + pc.li];
+    rng.v1 = P.rng[2 * pc.npix + pc.li];
+    rng.v2 = P.rng[3 * pc.npix + pc.li];
+    rng.v3 = P.rng[4 * pc.npix + pc.li];
+    rng.v4 = P.rng[5 * pc.npix + pc.li];
+    const float4 acc = P.accum[pc.li];
+    ps.accum = mk(acc.x, acc.y, acc.z);
+    ps.color = splat(0.0f);
+    ps.L = splat(0.0f);
+    ps.T = splat(1.0f);
+    ps.s = ps.c = ps.bounce = 0;
+    ps.alive = P.chunks > 0 && P.spp > 0;
+}
+
+PT_DEV void store_pixel(const TraceParams& P, const PixelCtx& pc, const Xorwow& rng, const PathState& ps)
+{
+    P.accum[pc.li] = make_float4(ps.accum.x, ps.accum.y, ps.accum.z, 1.0f);
+    P.rng[pc.li] = rng.d;
+    P.rng[pc.npix + pc.li] = rng.v0;
+    P.rng[2 * pc.npix + pc.li] = rng.v1;
+    P.rng[3 * pc.npix + pc.li] = rng.v2;
+    P.rng[4 * pc.npix + pc.li] = rng.v3;
+    P.rng[5 * pc.npix + pc.li] = rng.v4;
+}
+
+// ---------------------------------------------------------------------------------------------
+// Kernel A: lane-synchronous segments (traverse, then shade), per-lane path regeneration.
 // LDS layout per workgroup: [scene nodes (2 float4 each) | scene prims (4 float4 each)] when
 // SCENE_LDS, then WPB wave stacks of stackDepth x 64 u32.
-template <bool STATS, bool SCENE_LDS, int WPB>
-__global__ void __launch_bounds__(WPB * 64) trace_kernel(TraceParams P)
+// ---------------------------------------------------------------------------------------------
+// SL = 0: scene read through the caches; 1: BVH nodes staged in LDS; 2: nodes and primitives in LDS.
+template <bool STATS, int SL, int WPB, bool WW, int MINW>
+__global__ void __launch_bounds__(WPB * 64, MINW) trace_kernel(TraceParams P)
 {
     extern __shared__ float4 lds4[];
     const uint32_t lane = threadIdx.x & 63u;
     const uint32_t wave = threadIdx.x >> 6;
-    const uint32_t tile = blockIdx.x * (uint32_t)WPB + wave;
-    const uint32_t sceneF4 = SCENE_LDS ? 2u * P.nodeCount + 4u * P.primCount : 0u;
-    if (SCENE_LDS) {
+    const uint32_t sceneF4 = (SL >= 1 ? 2u * P.nodeCount : 0u) + (SL >= 2 ? 4u * P.primCount : 0u);
+    if (SL >= 1) {
         for (uint32_t i = threadIdx.x; i < 2u * P.nodeCount; i += WPB * 64) lds4[i] = P.nodes[i];
-        for (uint32_t i = threadIdx.x; i < 4u * P.primCount; i += WPB * 64) lds4[2u * P.nodeCount + i] = P.prims[i];
+        if (SL >= 2)
+            for (uint32_t i = threadIdx.x; i < 4u * P.primCount; i += WPB * 64) lds4[2u * P.nodeCount + i] = P.prims[i];
         __syncthreads();
     }
-    const float4* __restrict__ nodes = SCENE_LDS ? lds4 : P.nodes;
-    const float4* __restrict__ prims = SCENE_LDS ? lds4 + 2u * P.nodeCount : P.prims;
+    const float4* __restrict__ nodes = SL >= 1 ? lds4 : P.nodes;
+    const float4* __restrict__ prims = SL >= 2 ? lds4 + 2u * P.nodeCount : P.prims;
     uint32_t* stack = reinterpret_cast<uint32_t*>(lds4 + sceneF4) + wave * P.stackDepth * 64u + lane;
-    const uint32_t tileX = tile % P.tilesX, tileY = tile / P.tilesX;
-    const uint32_t px = tileX * 8u + (lane & 7u);
-    const uint32_t ly = tileY * 8u + (lane >> 3);
-    const bool valid = tileY < P.tilesY && px < P.width && ly < P.rows;
-    Counters cnt = {0, 0, 0, 0, 0, 0};
-    if (valid) {
-        const uint32_t py = P.rowOffset + ly * P.rowStride;
-        const size_t npix = (size_t)P.rows * P.width;
-        const size_t li = (size_t)ly * P.width + px;
+    const PixelCtx pc = pixel_of(P, blockIdx.x * (uint32_t)WPB + wave, lane);
+    Counters cnt = {};
+    if (pc.valid) {
         Xorwow rng;
-        rng.d = P.rng[li];
-        rng.v0 = P.rng[npix + li];
-        rng.v1 = P.rng[2 * npix + li];
-        rng.v2 = P.rng[3 * npix + li];
-        rng.v3 = P.rng[4 * npix + li];
-        rng.v4 = P.rng[5 * npix + li];
-        float4 acc = P.accum[li];
-        f3 accum = mk(acc.x, acc.y, acc.z);
-        const float fx = (float)(int32_t)px, fy = (float)(int32_t)py;
-        const float fw = (float)P.width, fh = (float)P.height;
-
-        f3 color = splat(0.0f);       // trace.cu:186 per-chunk sum
-        f3 L = splat(0.0f), T = splat(1.0f);
-        f3 o, d;
-        uint32_t s = 0, c = 0, bounce = 0;
-        bool alive = P.chunks > 0 && P.spp > 0;
-
-        // camera ray of the first sample (trace.cu:190-192, Camera.inl:25-28)
-        {
-            const float u = (fx + uniform(rng)) / fw;
-            const float v = (fy + uniform(rng)) / fh;
-            o = P.cam.origin;
-            d = normalize(add(add(P.cam.llc, scale(u, P.cam.horizontal)), scale(v, P.cam.vertical)));
-        }
-        while (alive) {
-            if (STATS) cnt.segments++;
+        PathState ps;
+        load_pixel(P, pc, rng, ps);
+        const float fx = (float)(int32_t)pc.px, fy = (float)(int32_t)pc.py;
+        camera_ray(P, fx, fy, rng, ps.o, ps.d);
+        while (ps.alive) {
+            if (STATS) { cnt.segments++; wave_tick(cnt.w_segments); }
             float t;
-            const uint32_t e = traverse<STATS>(nodes, prims, stack, o, d, t, cnt);
-            bool pathEnd;
-            if (e == 0xffffffffu) {                                       // trace.cu:115-134
-                f3 sky = splat(0.0f);
-                if (P.skybox != 0) {
-                    if (STATS) cnt.sky++;
-                    const float theta = acos_(d.y);
-                    const float phi = atan2_(d.z, d.x);
-                    const float v = theta / kPi;
-                    const float u = phi / kTwoPi;
-                    sky = tex2d(P.textures[P.skybox - 1], u, v);
+            const uint32_t e = traverse<STATS, WW>(nodes, prims, stack, ps.o, ps.d, P.slabFast != 0, t, cnt);
+            if (shade<STATS>(P, prims, e, t, ps, rng, cnt)) finish_path<STATS>(P, ps, rng, fx, fy, cnt);
+        }
+        store_pixel(P, pc, rng, ps);
+    }
+    flush_counters<STATS>(P, cnt);
+}
+
+// ---------------------------------------------------------------------------------------------
+// Kernel B: wave-scheduled state machine.  Every lane is in one of NODE (walking interior
+// nodes), LEAF (testing the primitives of a leaf, one per step), SHADE (traversal finished) or
+// DONE.  Each iteration the wave counts its lanes per state with __ballot and runs exactly one
+// phase for the lanes in that state: shading once SHADE_T lanes wait for it (or nothing else is
+// left), leaf tests once LEAF_T lanes wait (or no lane is walking nodes), node steps otherwise.
+// Every lane still performs the reference's sequence of node tests, primitive tests and shading
+// steps in order -- only the interleaving across lanes changes -- so results are bit-identical.
+// ---------------------------------------------------------------------------------------------
+enum : uint32_t { ST_NODE = 0, ST_LEAF = 1, ST_SHADE = 2, ST_DONE = 3 };
+
+template <bool STATS, int MINW, int SHADE_T, int LEAF_T>
+__global__ void __launch_bounds__(256, MINW) trace_sched_kernel(TraceParams P)
+{
+    extern __shared__ float4 lds4[];
+    const uint32_t lane = threadIdx.x & 63u;
+    const uint32_t wave = threadIdx.x >> 6;
+    const float4* __restrict__ nodes = P.nodes;
+    const float4* __restrict__ prims = P.prims;
+    uint32_t* stack = reinterpret_cast<uint32_t*>(lds4) + wave * P.stackDepth * 64u + lane;
+    const PixelCtx pc = pixel_of(P, blockIdx.x * 4u + wave, lane);
+    Counters cnt = {};
+    Xorwow rng = {};
+    PathState ps = {};
+    const float fx = (float)(int32_t)pc.px, fy = (float)(int32_t)pc.py;
+    const float tMin = 0.001f;
+    // traversal state (hitBVH, trace.cu:28-98)
+    float tMax = kFltMax, ix = 0.0f, iy = 0.0f, iz = 0.0f;
+    uint32_t cur = 0, sp = 0, elem = 0xffffffffu, leafOff = 0, leafCnt = 0, negMask = 0;
+    uint32_t state = ST_DONE;
+    if (pc.valid) {
+        load_pixel(P, pc, rng, ps);
+        if (ps.alive) {
+            camera_ray(P, fx, fy, rng, ps.o, ps.d);
+            state = ST_NODE;
+        }
+    }
+    bool fresh = true;   // a new ray needs its traversal set up
+    while (true) {
+        if (state == ST_NODE && fresh) {
+            ix = 1.0f / ps.d.x;
+            iy = 1.0f / ps.d.y;
+            iz = 1.0f / ps.d.z;
+            negMask = (ps.d.x < 0.0f ? 1u : 0u) | (ps.d.y < 0.0f ? 2u : 0u) | (ps.d.z < 0.0f ? 4u : 0u);
+            tMax = kFltMax;
+            cur = 0;
+            sp = 0;
+            elem = 0xffffffffu;
+            fresh = false;
+            if (STATS) { cnt.segments++; wave_tick(cnt.w_segments); }
+        }
+        const unsigned long long mN = __ballot(state == ST_NODE);
+        const unsigned long long mL = __ballot(state == ST_LEAF);
+        const unsigned long long mS = __ballot(state == ST_SHADE);
+        if ((mN | mL | mS) == 0ull) break;
+        const int nN = __popcll(mN), nL = __popcll(mL), nS = __popcll(mS);
+        if (nS >= SHADE_T || (nN + nL) == 0) {
+            if (state == ST_SHADE) {
+                if (shade<STATS>(P, prims, elem, tMax, ps, rng, cnt)) finish_path<STATS>(P, ps, rng, fx, fy, cnt);
+                state = ps.alive ? ST_NODE : ST_DONE;
+                fresh = true;
+            }
+        } else if (nL >= LEAF_T || nN == 0) {
+            if (state == ST_LEAF) {
+                if (STATS) { cnt.prim_tests++; wave_tick(cnt.w_prim); }
+                float t;
+                if (prim_hit(prims, leafOff, ps.o, ps.d, tMin, tMax, t)) {
+                    tMax = t;
+                    elem = leafOff;
                 }
-                L = add(L, mul(T, sky));
-                pathEnd = true;
-            } else {
-                if (STATS) cnt.hits++;
-                const float4 m0 = P.mats[3 * e + 0];
-                const float4 m1 = P.mats[3 * e + 1];
-                L = add(L, mul(T, mk(m1.x, m1.y, m1.z)));                 // trace.cu:139
-                if (bounce == 4) {
-                    // 5th segment: its scattered ray is discarded (trace.cu:109), only the two
-                    // uniforms of Material.inl:40-41 are observable.
-                    (void)uniform(rng);
-                    (void)uniform(rng);
-                    pathEnd = true;
-                } else {
-                    const float4 m2 = P.mats[3 * e + 2];
-                    const uint32_t texIdx = __float_as_uint(m2.x);
-                    const uint32_t mtype = __float_as_uint(m2.y);
-                    const Surface sf = surface_of(prims, e, o, d, t, texIdx != 0);
-                    f3 tg, bt;
-                    tangent_frame(sf.n, tg, bt);
-                    const f3 wo = neg(d);                                 // MonteCarlo.h:21
-                    const f3 V = normalize(add(add(scale(wo.x, mk(tg.x, bt.x, sf.n.x)), scale(wo.y, mk(tg.y, bt.y, sf.n.y))),
-                                               scale(wo.z, mk(tg.z, bt.z, sf.n.z))));
-                    f3 base = mk(m0.x, m0.y, m0.z);
-                    if (texIdx != 0) {                                    // Material.inl:26-35
-                        const f3 tap = tex2d(P.textures[texIdx - 1], sf.u, sf.v);
-                        base = mk(pow_(tap.x, 2.2f), pow_(tap.y, 2.2f), pow_(tap.z, 2.2f));
-                    }
-                    float rnd0 = uniform(rng);
-                    const float rnd1 = uniform(rng);
-                    const float rough = m0.w, metal = m1.w;
-                    const float a = rough * rough;
-                    const float a2 = a * a;
-                    f3 dir = splat(0.0f), att = splat(0.0f);
-                    float pdf = 0.0f;
-                    bool killed = false;
-                    if (mtype == 0u) {                                    // LAMBERT (Material.inl:67-72)
-                        dir = cosine_sample(rnd0, rnd1);
-                        pdf = dir.z / kPi;
-                        att = scale(kInvPi, base);
-                    } else if (mtype <= 2u) {
-                        bool specular = true;
-                        if (mtype == 2u) {                                // LAMBERT_GGX (:101-144)
-                            if (rnd0 < 0.5f) { rnd0 = 2.0f * rnd0; specular = false; }
-                            else rnd0 = 2.0f * (rnd0 - 0.5f);
-                        }
-                        if (specular) dir = reflect(neg(V), vndf_sample(V, rnd0, rnd1, a));
-                        else dir = cosine_sample(rnd0, rnd1);
-                        if (dir.z < 0.0f) {
-                            killed = true;                                // pdf = 1, attenuation 0
-                        } else {
-                            const float NdotV = fabsf(V.z) + 1e-5f;
-                            const f3 H = normalize(add(V, dir));
-                            const float VdotH = clamp01(dot(V, H));
-                            const float NdotH = clamp01(H.z);
-                            const float NdotL = clamp01(dir.z);
-                            const float ggxPdf = vndf_pdf(H, V, a);
-                            const f3 F0 = lerp(splat(0.04f), base, metal);
-                            const f3 kS = specular_ggx(F0, NdotV, NdotL, NdotH, VdotH, a2);
-                            if (mtype == 1u) {                            // GGX (:74-99)
-                                pdf = ggxPdf;
-                                att = kS;
-                            } else {
-                                const float cosinePdf = dir.z / kPi;
-                                pdf = (ggxPdf + cosinePdf) * 0.5f;
-                                att = add(scale(1.0f - metal, scale(kInvPi, base)), kS);
-                            }
-                        }
-                    }
-                    if (killed || is_zero(att) || pdf == 0.0f) {          // trace.cu:145-148
-                        pathEnd = true;
-                    } else {
-                        // Material.inl:57: normalize(tangentToWorld(...)), which itself normalizes
-                        const f3 sd = normalize(normalize(add(add(scale(dir.x, tg), scale(dir.y, bt)), scale(dir.z, sf.n))));
-                        const f3 w = divs(scale(fabsf(dot(sd, sf.n)), att), pdf);   // trace.cu:150
-                        T = mul(T, w);
-                        o = sf.p;
-                        d = sd;
-                        ++bounce;
-                        pathEnd = false;
-                    }
+                ++leafOff;
+                if (--leafCnt == 0) {
+                    if (sp == 0) state = ST_SHADE;
+                    else { cur = stack[64u * (--sp)]; state = ST_NODE; }
                 }
             }
-            if (pathEnd) {
-                color = add(color, L);                                    // trace.cu:193
-                if (STATS) cnt.samples++;
-                if (++s == P.spp) {
-                    const bool ignore = (c == 0) && P.ignoreFirst;       // trace.cu:196
-                    accum = ignore ? color : add(color, accum);
-                    color = splat(0.0f);
-                    s = 0;
-                    if (++c == P.chunks) alive = false;
-                }
-                if (alive) {
-                    const float u = (fx + uniform(rng)) / fw;
-                    const float v = (fy + uniform(rng)) / fh;
-                    o = P.cam.origin;
-                    d = normalize(add(add(P.cam.llc, scale(u, P.cam.horizontal)), scale(v, P.cam.vertical)));
-                    L = splat(0.0f);
-                    T = splat(1.0f);
-                    bounce = 0;
+        } else {
+            if (state == ST_NODE) {
+                if (STATS) { cnt.node_tests++; wave_tick(cnt.w_node); }
+                const NodeHit nh = node_test(nodes, cur, ps.o, ix, iy, iz, tMin, tMax);
+                if (nh.hit) {
+                    const uint32_t count = nh.pca >> 16;
+                    if (count > 0) {
+                        leafOff = nh.offset;
+                        leafCnt = count;
+                        state = ST_LEAF;
+                    } else {
+                        const uint32_t axis = (nh.pca >> 8) & 0xffu;
+                        const bool isNeg = (negMask >> axis) & 1u;
+                        stack[64u * (sp++)] = isNeg ? (cur + 1) : nh.offset;
+                        cur = isNeg ? nh.offset : (cur + 1);
+                    }
+                } else {
+                    if (sp == 0) state = ST_SHADE;
+                    else cur = stack[64u * (--sp)];
                 }
             }
         }
-        if (P.chunks > 0 && P.spp > 0) P.accum[li] = make_float4(accum.x, accum.y, accum.z, 1.0f);
-        P.rng[li] = rng.d;
-        P.rng[npix + li] = rng.v0;
-        P.rng[2 * npix + li] = rng.v1;
-        P.rng[3 * npix + li] = rng.v2;
-        P.rng[4 * npix + li] = rng.v3;
-        P.rng[5 * npix + li] = rng.v4;
     }
-    if (STATS) {
-        atomicAdd(&P.stats[0], (unsigned long long)cnt.node_tests);
-        atomicAdd(&P.stats[1], (unsigned long long)cnt.prim_tests);
-        atomicAdd(&P.stats[2], (unsigned long long)cnt.hits);
-        atomicAdd(&P.stats[3], (unsigned long long)cnt.sky);
-        atomicAdd(&P.stats[4], (unsigned long long)cnt.segments);
-        atomicAdd(&P.stats[5], (unsigned long long)cnt.samples);
-    }
+    if (pc.valid) store_pixel(P, pc, rng, ps);
+    flush_counters<STATS>(P, cnt);
 }
 
 // initRandState (initRandState.cu:4-17): curand_init(1984 + x + y * width, 0, 0)
@@ -645,6 +914,7 @@ struct pt_context {
     float4* prims = nullptr;
     float4* mats = nullptr;
     uint32_t nodeCount = 0, primCount = 0, stackDepth = 1;
+    bool slabFast = true;
     int variant = 0;
     DevTex* texTable = nullptr;
     DevTex hostTex[PT_MAX_TEXTURES] = {};
@@ -683,22 +953,32 @@ static int fail(pt_context* ctx, int code, const char* msg)
 }
 
 // Kernel variants (workgroup size, scene staged in LDS or read through the caches).
-template <bool STATS, bool SL, int WPB>
+template <bool STATS, int SL, int WPB, bool WW, int MINW>
 static hipError_t launch_one(const TraceParams& P, hipStream_t stream)
 {
-    const size_t sceneBytes = SL ? (2 * (size_t)P.nodeCount + 4 * (size_t)P.primCount) * sizeof(float4) : 0;
+    const size_t sceneBytes = ((SL >= 1 ? 2 * (size_t)P.nodeCount : 0) + (SL >= 2 ? 4 * (size_t)P.primCount : 0)) * sizeof(float4);
     const size_t lds = sceneBytes + (size_t)WPB * P.stackDepth * 64 * sizeof(uint32_t);
     if (lds > 160 * 1024) return hipErrorInvalidValue;
     static bool attrSet = false;
     if (!attrSet) {
-        hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(&trace_kernel<STATS, SL, WPB>),
+        hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(&trace_kernel<STATS, SL, WPB, WW, MINW>),
                                            hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
         if (e != hipSuccess) return e;
         attrSet = true;
     }
     const uint32_t tiles = P.tilesX * P.tilesY;
     const unsigned blocks = (tiles + WPB - 1) / WPB;
-    trace_kernel<STATS, SL, WPB><<<blocks, WPB * 64, lds, stream>>>(P);
+    trace_kernel<STATS, SL, WPB, WW, MINW><<<blocks, WPB * 64, lds, stream>>>(P);
+    return hipGetLastError();
+}
+
+template <bool STATS, int MINW, int SHADE_T, int LEAF_T>
+static hipError_t launch_sched(const TraceParams& P, hipStream_t stream)
+{
+    const size_t lds = (size_t)4 * P.stackDepth * 64 * sizeof(uint32_t);
+    const uint32_t tiles = P.tilesX * P.tilesY;
+    const unsigned blocks = (tiles + 3) / 4;
+    trace_sched_kernel<STATS, MINW, SHADE_T, LEAF_T><<<blocks, 256, lds, stream>>>(P);
     return hipGetLastError();
 }
 
@@ -706,20 +986,27 @@ template <bool STATS>
 static hipError_t launch_variant(int v, const TraceParams& P, hipStream_t stream)
 {
     switch (v) {
-    case 1: return launch_one<STATS, false, 4>(P, stream);
-    case 2: return launch_one<STATS, true, 4>(P, stream);
-    case 3: return launch_one<STATS, true, 8>(P, stream);
-    case 4: return launch_one<STATS, true, 16>(P, stream);
-    case 5: return launch_one<STATS, false, 16>(P, stream);
-    default: return launch_one<STATS, true, 8>(P, stream);
+    case 1: return launch_one<STATS, 0, 4, false, 1>(P, stream);
+    case 2: return launch_one<STATS, 1, 4, false, 1>(P, stream);
+    case 3: return launch_one<STATS, 0, 4, true, 1>(P, stream);
+    case 4: return launch_one<STATS, 0, 4, true, 5>(P, stream);
+    case 5: return launch_one<STATS, 1, 4, true, 1>(P, stream);
+    case 6: return launch_one<STATS, 1, 4, true, 5>(P, stream);
+    case 7: return launch_one<STATS, 1, 4, false, 5>(P, stream);
+    case 8: return launch_one<STATS, 2, 8, true, 1>(P, stream);
+    case 9: return launch_sched<STATS, 1, 32, 16>(P, stream);
+    default: return launch_one<STATS, 0, 4, true, 1>(P, stream);
     }
 }
 
 static int pick_variant(const pt_context* ctx)
 {
     if (ctx->variant > 0) return ctx->variant;
-    const size_t sceneBytes = (2 * (size_t)ctx->nodeCount + 4 * (size_t)ctx->primCount) * sizeof(float4);
-    return sceneBytes <= 96 * 1024 ? 3 : 5;
+    // measured on MI355X (tools/ab_variants.py, profiles/): staging the BVH nodes in LDS cuts the
+    // latency of the dependent node fetches; while-while traversal + 5 waves/SIMD win on the
+    // 484-object scene.  Large BVHs (e.g. the 100k-object stress scene) stay in global memory.
+    const size_t nodeBytes = 2 * (size_t)ctx->nodeCount * sizeof(float4);
+    return nodeBytes <= 48 * 1024 ? 6 : 4;
 }
 
 extern "C" {
@@ -757,7 +1044,7 @@ PT_API int pt_create(int device, uint32_t width, uint32_t height, uint32_t row_o
     if (hipMalloc(&ctx->accum, nalloc * sizeof(float4)) != hipSuccess) return bail(PT_ERR_HIP);
     if (hipMalloc(&ctx->rng, nalloc * 6 * sizeof(uint32_t)) != hipSuccess) return bail(PT_ERR_HIP);
     if (hipMalloc(&ctx->texTable, PT_MAX_TEXTURES * sizeof(DevTex)) != hipSuccess) return bail(PT_ERR_HIP);
-    if (hipMalloc(&ctx->stats, 8 * sizeof(unsigned long long)) != hipSuccess) return bail(PT_ERR_HIP);
+    if (hipMalloc(&ctx->stats, 16 * sizeof(unsigned long long)) != hipSuccess) return bail(PT_ERR_HIP);
     if (hipMemsetAsync(ctx->accum, 0, nalloc * sizeof(float4), ctx->stream) != hipSuccess) return bail(PT_ERR_HIP);
     if (hipMemcpyAsync(ctx->texTable, ctx->hostTex, sizeof(ctx->hostTex), hipMemcpyHostToDevice, ctx->stream) != hipSuccess)
         return bail(PT_ERR_HIP);
@@ -835,17 +1122,20 @@ PT_API int pt_set_scene(pt_context* ctx, const pt_bvh_node* nodes, uint32_t node
     int rc = validate_scene(ctx, nodes, node_count, prims, prim_count, maxDepth);
     if (rc != PT_OK) return rc;
     std::vector<float4> hn(2 * (size_t)node_count), hp(4 * (size_t)prim_count), hm(3 * (size_t)prim_count);
+    bool slabFast = true;
     for (uint32_t i = 0; i < node_count; ++i) {
         const pt_bvh_node& n = nodes[i];
-        hn[2 * i] = make_float4(n.aabb_min[0], n.aabb_min[1], n.aabb_min[2], n.aabb_max[0]);
-        hn[2 * i + 1] = make_float4(n.aabb_max[1], n.aabb_max[2], u2f(n.offset),
-                                    u2f(n.primitive_count_axis));
+        hn[2 * i] = make_float4(n.aabb_min[0], n.aabb_max[0], n.aabb_min[1], n.aabb_max[1]);
+        hn[2 * i + 1] = make_float4(n.aabb_min[2], n.aabb_max[2], u2f(n.offset), u2f(n.primitive_count_axis));
+        for (int k = 0; k < 3; ++k)   // the fast slab test needs ordered, non-NaN bounds
+            if (!(n.aabb_min[k] <= n.aabb_max[k])) slabFast = false;
     }
     for (uint32_t i = 0; i < prim_count; ++i) {
         const pt_hittable& h = prims[i];
-        for (int r = 0; r < 3; ++r)
-            hp[4 * i + r] = make_float4(h.inv_transform_rows[r][0], h.inv_transform_rows[r][1], h.inv_transform_rows[r][2],
-                                        h.inv_transform_rows[r][3]);
+        const float(&R)[3][4] = h.inv_transform_rows;
+        hp[4 * i + 0] = make_float4(R[0][0], R[1][0], R[0][1], R[1][1]);
+        hp[4 * i + 1] = make_float4(R[0][2], R[1][2], R[0][3], R[1][3]);
+        hp[4 * i + 2] = make_float4(R[2][0], R[2][1], R[2][2], R[2][3]);
         hp[4 * i + 3] = make_float4(u2f(h.type), 0.0f, 0.0f, 0.0f);
         hm[3 * i] = make_float4(h.base_color[0], h.base_color[1], h.base_color[2], h.roughness);
         hm[3 * i + 1] = make_float4(h.emissive[0], h.emissive[1], h.emissive[2], h.metalness);
@@ -866,6 +1156,7 @@ PT_API int pt_set_scene(pt_context* ctx, const pt_bvh_node* nodes, uint32_t node
     PT_HIP_CHECK(ctx, hipMemcpy(ctx->mats, hm.data(), hm.size() * sizeof(float4), hipMemcpyHostToDevice));
     ctx->nodeCount = node_count;
     ctx->primCount = prim_count;
+    ctx->slabFast = slabFast;
     // a traversal holds at most one pending sibling per interior ancestor: depth - 1 entries
     ctx->stackDepth = maxDepth > 1 ? maxDepth - 1 : 1;
     return PT_OK;
@@ -938,7 +1229,8 @@ static int render_impl(pt_context* ctx, const pt_camera* cam, uint32_t spp, uint
     P.nodeCount = ctx->nodeCount;
     P.primCount = ctx->primCount;
     P.stackDepth = ctx->stackDepth;
-    if (stats) PT_HIP_CHECK(ctx, hipMemsetAsync(ctx->stats, 0, 8 * sizeof(unsigned long long), ctx->stream));
+    P.slabFast = ctx->slabFast ? 1u : 0u;
+    if (stats) PT_HIP_CHECK(ctx, hipMemsetAsync(ctx->stats, 0, 16 * sizeof(unsigned long long), ctx->stream));
     PT_HIP_CHECK(ctx, hipEventRecord(ctx->ev0, ctx->stream));
     const int variant = pick_variant(ctx);
     PT_HIP_CHECK(ctx, stats ? launch_variant<true>(variant, P, ctx->stream) : launch_variant<false>(variant, P, ctx->stream));
@@ -949,7 +1241,7 @@ static int render_impl(pt_context* ctx, const pt_camera* cam, uint32_t spp, uint
     PT_HIP_CHECK(ctx, hipEventElapsedTime(&ms, ctx->ev0, ctx->ev1));
     if (gpu_ms) *gpu_ms = ms;
     if (stats) {
-        unsigned long long h[8];
+        unsigned long long h[16];
         PT_HIP_CHECK(ctx, hipMemcpy(h, ctx->stats, sizeof(h), hipMemcpyDeviceToHost));
         stats->node_tests = h[0];
         stats->prim_tests = h[1];
@@ -957,6 +1249,11 @@ static int render_impl(pt_context* ctx, const pt_camera* cam, uint32_t spp, uint
         stats->sky_lookups = h[3];
         stats->segments = h[4];
         stats->samples = h[5];
+        stats->wave_node_iters = h[6];
+        stats->wave_prim_iters = h[7];
+        stats->wave_hits = h[8];
+        stats->wave_sky = h[9];
+        stats->wave_segments = h[10];
     }
     return PT_OK;
 }
@@ -1041,7 +1338,7 @@ PT_API uint32_t pt_local_rows(const pt_context* ctx) { return ctx ? ctx->rows : 
 
 PT_API int pt_set_kernel_variant(pt_context* ctx, int variant)
 {
-    if (!ctx || variant < 0 || variant > 5) return PT_ERR_ARG;
+    if (!ctx || variant < 0 || variant > 9) return PT_ERR_ARG;
     ctx->variant = variant;
     return PT_OK;
 }

@@ -67,6 +67,17 @@ def test_render_bitexact(gpu_available, scenes, name, W, H, spp, chunks):
     assert pt.frames == ref.frames == chunks
 
 
+@pytest.mark.parametrize("variant", range(1, 10))
+def test_every_kernel_variant_bitexact(gpu_available, scenes, variant):
+    # all trace-kernel variants (schedules, LDS staging, occupancy) produce the reference's bits
+    pt, cam, ref, osc = pair(scenes / "test_shapes.scene.json", 72, 40)
+    pt.set_kernel_variant(variant)
+    pt.render(cam, 4, True, chunks=2)
+    ref.render(osc.camera, 4, True, chunks=2)
+    assert_bitexact(pt.accum(), ref.accum, f"variant {variant}")
+    assert np.array_equal(pt.rng_state(), ref.rng_array())
+
+
 def test_history_semantics(gpu_available, scenes):
     # render(cam, spp, ignoreHistory) sequence: trace.cu:196 and Pathtracer.cpp:164-167,226
     pt, cam, ref, osc = pair(scenes / "test_shapes.scene.json", 48, 40)

@@ -1,0 +1,30 @@
+"""SIMD efficiency of each phase of the trace kernel (instrumented variant): lane-level events
+divided by 64 x wave-level executions.  Usage: python tools/simd_eff.py [--scene ...] [--variant N]"""
+import argparse
+import json
+import pathlib
+import sys
+
+ROOT = pathlib.Path(__file__).resolve().parents[1]
+sys.path.insert(0, str(ROOT))
+import pathtracercuda_amd as pa  # noqa: E402
+
+ap = argparse.ArgumentParser()
+ap.add_argument("--scene", default=str(ROOT / "scenes/generated_scene.scene.json"))
+ap.add_argument("--width", type=int, default=1920)
+ap.add_argument("--height", type=int, default=1080)
+ap.add_argument("--variants", default="1,3")
+a = ap.parse_args()
+pt = pa.Pathtracer(a.width, a.height)
+cam = pt.load_scene(a.scene)
+res = {}
+for v in [int(x) for x in a.variants.split(",")]:
+    pt.set_kernel_variant(v)
+    st = pt.render_instrumented(cam, 8, 1, True)
+    eff = {k: round(st[l] / (64.0 * st[w]), 3) if st[w] else None for k, l, w in [
+        ("node", "node_tests", "wave_node_iters"), ("prim", "prim_tests", "wave_prim_iters"),
+        ("hit_shade", "hits", "wave_hits"), ("sky", "sky_lookups", "wave_sky"), ("segment", "segments", "wave_segments")]}
+    per_sample = {k: round(st[k] / st["samples"], 3) for k in ("node_tests", "prim_tests", "hits", "sky_lookups", "segments",
+                                                                "wave_node_iters", "wave_prim_iters", "wave_hits", "wave_sky", "wave_segments")}
+    res[v] = {"simd_efficiency": eff, "per_sample": per_sample}
+print(json.dumps({"scene": pathlib.Path(a.scene).name, "variants": res}, indent=1))
