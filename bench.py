@@ -110,14 +110,12 @@ def main():
         recv = [torch.zeros_like(send) for _ in range(n)] if rank == 0 else None
         full = torch.empty((H, W, 4), dtype=torch.float32, device=f"cuda:{local_rank}") if rank == 0 else None
 
+    from pathtracercuda_amd.distributed import gather_framebuffer
+
     def gather():
         # RCCL framebuffer gather over xGMI + unpermute of the interleaved rows on rank 0
         pt.copy_accum_to_device(send.data_ptr(), send.numel() * 4)
-        dist.gather(send, recv, dst=0)
-        if rank == 0:
-            for r in range(n):
-                rows_r = (H - r + n - 1) // n
-                full[r::n] = recv[r][:rows_r]
+        gather_framebuffer(send, H, rank, n, recv=recv, full=full)
 
     def step():
         ms = pt.render_raw(cam, chunk, chunks, True)
