@@ -1,0 +1,38 @@
+"""Turn the rocprofv3 --pmc passes of the bench command into profiles/<tag>_pmc_traffic.json:
+per-launch HBM bytes of the timed trace_kernel dispatch, FETCH_SIZE x 2 (gfx950 reports half of a
+wide coalesced read, MI355X_MICROARCH.md §HBM) + WRITE_SIZE, both KiB -> bytes."""
+import json
+import pathlib
+import subprocess
+import sys
+
+ROOT = pathlib.Path(__file__).resolve().parents[1]
+sys.path.insert(0, str(ROOT / "tools"))
+from pmc_summary import load  # noqa: E402
+
+
+def main():
+    src = pathlib.Path(sys.argv[1]) if len(sys.argv) > 1 else ROOT / "gpurun_out" / "pmc_bench"
+    tag = sys.argv[2] if len(sys.argv) > 2 else "r01"
+    disp, names = load(src, "trace_kernel<false")
+    best = {}
+    for (p, i), c in disp.items():
+        if p not in best or c.get("DURATION_NS", 0) > best[p].get("DURATION_NS", 0):
+            best[p] = c
+    merged = {}
+    for p, c in sorted(best.items()):
+        merged.update({k: v for k, v in c.items() if k != "DURATION_NS"})
+        merged.setdefault("duration_ns", c.get("DURATION_NS"))
+    fetch, write = merged.get("FETCH_SIZE"), merged.get("WRITE_SIZE")
+    out = {"workload": "generated_scene 1920x1080 1024spp chunk8", "kernel": "trace_kernel (timed launch)",
+           "fetch_size_kib": fetch, "write_size_kib": write,
+           "bytes_per_launch": (2 * fetch + write) * 1024 if fetch is not None and write is not None else None,
+           "correction": "FETCH_SIZE x2 (gfx950 reports half of wide coalesced reads); KiB -> bytes",
+           "counters": merged}
+    dst = ROOT / "profiles" / f"{tag}_pmc_traffic.json"
+    dst.write_text(json.dumps(out, indent=1, sort_keys=True) + "\n")
+    print(f"wrote {dst}: {out['bytes_per_launch']}")
+
+
+if __name__ == "__main__":
+    main()
