@@ -87,6 +87,12 @@ typedef struct pt_render_stats {
     uint64_t wave_hits;
     uint64_t wave_sky;
     uint64_t wave_segments;
+    /* shader-clock cycles summed over waves (s_memtime stamps; while-while variants): interior
+     * walk, leaf tests, shading, whole lane loop */
+    uint64_t cycles_node_walk;
+    uint64_t cycles_leaf_tests;
+    uint64_t cycles_shading;
+    uint64_t cycles_total;
 } pt_render_stats;
 
 typedef struct pt_context pt_context;
@@ -148,8 +154,9 @@ PT_API int pt_write_rng(pt_context *ctx, const uint32_t *src);
 
 PT_API uint32_t pt_local_rows(const pt_context *ctx);
 
-/* Tuning knob for A/B measurements: 0 = automatic (default); 1..5 select a trace-kernel variant
- * (workgroup size, scene staged in LDS or read through the caches).  Results are identical. */
+/* Tuning knob for A/B measurements: 0 = automatic (default); 1..18 select a trace-kernel variant
+ * (workgroup size, BVH/primitives staged in LDS or read through the caches, traversal loop shape,
+ * occupancy target).  All variants produce bit-identical results. */
 PT_API int pt_set_kernel_variant(pt_context *ctx, int variant);
 PT_API const char *pt_last_error(const pt_context *ctx);
 

@@ -210,7 +210,18 @@ struct Counters {
     uint32_t node_tests, prim_tests, hits, sky, segments, samples;
     // wave-level executions of the same points (SIMD efficiency = lane count / (64 * wave count))
     uint32_t w_node, w_prim, w_hits, w_sky, w_segments;
+    // wave-level shader-clock cycles per phase (instrumented variant only)
+    uint64_t cyc_node, cyc_leaf, cyc_shade, cyc_total;
 };
+
+// Adds the cycles since `t0` to `acc` once per wave and restarts the stamp.
+PT_DEV void wave_time(uint64_t& acc, uint64_t& t0)
+{
+    const uint64_t t = __builtin_amdgcn_s_memtime();
+    const unsigned long long m = __ballot(1);
+    if ((threadIdx.x & 63u) == (uint32_t)(__ffsll((long long)m) - 1)) acc += t - t0;
+    t0 = t;
+}
 
 // Counts one per wave that executes this point (instrumented variant only).
 PT_DEV void wave_tick(uint32_t& c)
@@ -289,7 +300,7 @@ PT_DEV NodeHit node_test_fast(const float4* __restrict__ nodes, uint32_t cur, f2
 // finishes); then the wave tests the pending leaves together.  The per-lane sequence of node and
 // primitive tests is unchanged -- only the SIMD schedule differs -- so results are bit-identical,
 // but the expensive primitive tests run with most lanes active instead of once per node step.
-template <bool STATS, bool WW>
+template <bool STATS, int WW>
 PT_DEV uint32_t traverse(const float4* __restrict__ nodes, const float4* __restrict__ prims, uint32_t* stack, f3 o,
                          f3 d, bool slabFast, float& tHit, Counters& cnt)
 {
@@ -306,7 +317,7 @@ PT_DEV uint32_t traverse(const float4* __restrict__ nodes, const float4* __restr
                     : node_test(nodes, node, o, ix, iy, iz, tMin, tMax);
     };
     uint32_t sp = 0, cur = 0, elem = 0xffffffffu;
-    if (!WW) {
+    if (WW == 0) {
         for (;;) {
             if (STATS) { cnt.node_tests++; wave_tick(cnt.w_node); }
             const NodeHit nh = test(cur);
@@ -333,9 +344,10 @@ PT_DEV uint32_t traverse(const float4* __restrict__ nodes, const float4* __restr
                 cur = stack[64u * (--sp)];
             }
         }
-    } else {
+    } else if (WW == 1) {
         uint32_t leafOff = 0, leafCnt = 0;
         bool done = false;
+        uint64_t tPhase = STATS ? __builtin_amdgcn_s_memtime() : 0;
         while (!done) {
             while (leafCnt == 0 && !done) {                     // interior walk
                 if (STATS) { cnt.node_tests++; wave_tick(cnt.w_node); }
@@ -358,6 +370,7 @@ PT_DEV uint32_t traverse(const float4* __restrict__ nodes, const float4* __restr
                     else cur = stack[64u * (--sp)];
                 }
             }
+            if (STATS) wave_time(cnt.cyc_node, tPhase);
             while (leafCnt > 0) {                                // pending leaf, in order
                 if (STATS) { cnt.prim_tests++; wave_tick(cnt.w_prim); }
                 float t;
@@ -368,7 +381,56 @@ PT_DEV uint32_t traverse(const float4* __restrict__ nodes, const float4* __restr
                 ++leafOff;
                 --leafCnt;
             }
+            if (STATS) wave_time(cnt.cyc_leaf, tPhase);
             if (!done) {
+                if (sp == 0) done = true;
+                else cur = stack[64u * (--sp)];
+            }
+        }
+    } else {
+        // threshold while-while: leave the interior walk as soon as WW lanes have a leaf pending
+        uint32_t leafOff = 0, leafCnt = 0;
+        bool done = false;
+        while (!done) {
+            for (;;) {
+                const bool walking = leafCnt == 0;
+                const unsigned long long mw = __ballot(walking);
+                const unsigned long long ml = __ballot(!walking);
+                if (mw == 0ull || __popcll(ml) >= WW) break;
+                if (walking) {
+                    if (STATS) { cnt.node_tests++; wave_tick(cnt.w_node); }
+                    const NodeHit nh = test(cur);
+                    const uint32_t count = nh.pca >> 16;
+                    const bool isNeg = (negMask >> ((nh.pca >> 8) & 0xffu)) & 1u;
+                    const uint32_t nearC = isNeg ? nh.offset : cur + 1;
+                    const uint32_t farC = isNeg ? cur + 1 : nh.offset;
+                    if (nh.hit) {
+                        if (count > 0) {
+                            leafOff = nh.offset;
+                            leafCnt = count;
+                        } else {
+                            stack[64u * sp] = farC;
+                            ++sp;
+                            cur = nearC;
+                        }
+                    } else {
+                        if (sp == 0) { done = true; break; }
+                        cur = stack[64u * (--sp)];
+                    }
+                }
+            }
+            if (done) break;
+            if (leafCnt > 0) {
+                while (leafCnt > 0) {
+                    if (STATS) { cnt.prim_tests++; wave_tick(cnt.w_prim); }
+                    float t;
+                    if (prim_hit(prims, leafOff, o, d, tMin, tMax, t)) {
+                        tMax = t;
+                        elem = leafOff;
+                    }
+                    ++leafOff;
+                    --leafCnt;
+                }
                 if (sp == 0) done = true;
                 else cur = stack[64u * (--sp)];
             }
@@ -384,12 +446,9 @@ struct Surface {
     float u, v;
 };
 
-PT_DEV Surface surface_of(const float4* __restrict__ prims, uint32_t e, f3 o, f3 d, float t, bool needUV)
+PT_DEV Surface surface_of(const float4& r0, const float4& r1, const float4& r2, uint32_t type, f3 o, f3 d, float t,
+                          bool needUV)
 {
-    const float4 r0 = prims[4 * e + 0];
-    const float4 r1 = prims[4 * e + 1];
-    const float4 r2 = prims[4 * e + 2];
-    const uint32_t type = __float_as_uint(prims[4 * e + 3].x);
     const LocalRay r = to_local(r0, r1, r2, o, d);
     const f3 lp = add(r.o, scale(t, r.d));                 // r.at(t) in object space
     f3 n;
@@ -552,8 +611,15 @@ PT_DEV bool shade(const TraceParams& P, const float4* __restrict__ prims, uint32
         return true;
     }
     if (STATS) { cnt.hits++; wave_tick(cnt.w_hits); }
+    // every load the hit needs is issued here, together: material, then the primitive's rows for
+    // rebuilding the hit record (the shading chain is latency-bound)
     const float4 m0 = P.mats[3 * e + 0];
     const float4 m1 = P.mats[3 * e + 1];
+    const float4 m2 = P.mats[3 * e + 2];
+    const float4 q0 = prims[4 * e + 0];
+    const float4 q1 = prims[4 * e + 1];
+    const float4 q2 = prims[4 * e + 2];
+    const uint32_t ptype = __float_as_uint(prims[4 * e + 3].x);
     ps.L = add(ps.L, mul(ps.T, mk(m1.x, m1.y, m1.z)));                      // trace.cu:139
     if (ps.bounce == 4) {
         // 5th segment: its scattered ray is discarded (trace.cu:109); only the two uniforms of
@@ -562,10 +628,9 @@ PT_DEV bool shade(const TraceParams& P, const float4* __restrict__ prims, uint32
         (void)uniform(rng);
         return true;
     }
-    const float4 m2 = P.mats[3 * e + 2];
     const uint32_t texIdx = __float_as_uint(m2.x);
     const uint32_t mtype = __float_as_uint(m2.y);
-    const Surface sf = surface_of(prims, e, ps.o, ps.d, t, texIdx != 0);
+    const Surface sf = surface_of(q0, q1, q2, ptype, ps.o, ps.d, t, texIdx != 0);
     f3 tg, bt;
     tangent_frame(sf.n, tg, bt);
     const f3 wo = neg(ps.d);                                                  // MonteCarlo.h:15-22
@@ -665,6 +730,10 @@ PT_DEV void flush_counters(const TraceParams& P, const Counters& cnt)
     atomicAdd(&P.stats[8], (unsigned long long)cnt.w_hits);
     atomicAdd(&P.stats[9], (unsigned long long)cnt.w_sky);
     atomicAdd(&P.stats[10], (unsigned long long)cnt.w_segments);
+    atomicAdd(&P.stats[11], (unsigned long long)cnt.cyc_node);
+    atomicAdd(&P.stats[12], (unsigned long long)cnt.cyc_leaf);
+    atomicAdd(&P.stats[13], (unsigned long long)cnt.cyc_shade);
+    atomicAdd(&P.stats[14], (unsigned long long)cnt.cyc_total);
 }
 
 struct PixelCtx {
@@ -720,7 +789,7 @@ PT_DEV void store_pixel(const TraceParams& P, const PixelCtx& pc, const Xorwow& 
 // SCENE_LDS, then WPB wave stacks of stackDepth x 64 u32.
 // ---------------------------------------------------------------------------------------------
 // SL = 0: scene read through the caches; 1: BVH nodes staged in LDS; 2: nodes and primitives in LDS.
-template <bool STATS, int SL, int WPB, bool WW, int MINW>
+template <bool STATS, int SL, int WPB, int WW, int MINW>
 __global__ void __launch_bounds__(WPB * 64, MINW) trace_kernel(TraceParams P)
 {
     extern __shared__ float4 lds4[];
@@ -744,12 +813,16 @@ __global__ void __launch_bounds__(WPB * 64, MINW) trace_kernel(TraceParams P)
         load_pixel(P, pc, rng, ps);
         const float fx = (float)(int32_t)pc.px, fy = (float)(int32_t)pc.py;
         camera_ray(P, fx, fy, rng, ps.o, ps.d);
+        uint64_t tAll = STATS ? __builtin_amdgcn_s_memtime() : 0;
         while (ps.alive) {
             if (STATS) { cnt.segments++; wave_tick(cnt.w_segments); }
             float t;
             const uint32_t e = traverse<STATS, WW>(nodes, prims, stack, ps.o, ps.d, P.slabFast != 0, t, cnt);
+            uint64_t tS = STATS ? __builtin_amdgcn_s_memtime() : 0;
             if (shade<STATS>(P, prims, e, t, ps, rng, cnt)) finish_path<STATS>(P, ps, rng, fx, fy, cnt);
+            if (STATS) wave_time(cnt.cyc_shade, tS);
         }
+        if (STATS) wave_time(cnt.cyc_total, tAll);
         store_pixel(P, pc, rng, ps);
     }
     flush_counters<STATS>(P, cnt);
@@ -953,7 +1026,7 @@ static int fail(pt_context* ctx, int code, const char* msg)
 }
 
 // Kernel variants (workgroup size, scene staged in LDS or read through the caches).
-template <bool STATS, int SL, int WPB, bool WW, int MINW>
+template <bool STATS, int SL, int WPB, int WW, int MINW>
 static hipError_t launch_one(const TraceParams& P, hipStream_t stream)
 {
     const size_t sceneBytes = ((SL >= 1 ? 2 * (size_t)P.nodeCount : 0) + (SL >= 2 ? 4 * (size_t)P.primCount : 0)) * sizeof(float4);
@@ -986,16 +1059,25 @@ template <bool STATS>
 static hipError_t launch_variant(int v, const TraceParams& P, hipStream_t stream)
 {
     switch (v) {
-    case 1: return launch_one<STATS, 0, 4, false, 1>(P, stream);
-    case 2: return launch_one<STATS, 1, 4, false, 1>(P, stream);
-    case 3: return launch_one<STATS, 0, 4, true, 1>(P, stream);
-    case 4: return launch_one<STATS, 0, 4, true, 5>(P, stream);
-    case 5: return launch_one<STATS, 1, 4, true, 1>(P, stream);
-    case 6: return launch_one<STATS, 1, 4, true, 5>(P, stream);
-    case 7: return launch_one<STATS, 1, 4, false, 5>(P, stream);
-    case 8: return launch_one<STATS, 2, 8, true, 1>(P, stream);
+    case 1: return launch_one<STATS, 0, 4, 0, 1>(P, stream);
+    case 2: return launch_one<STATS, 1, 4, 0, 1>(P, stream);
+    case 3: return launch_one<STATS, 0, 4, 1, 1>(P, stream);
+    case 4: return launch_one<STATS, 0, 4, 1, 5>(P, stream);
+    case 5: return launch_one<STATS, 1, 4, 1, 1>(P, stream);
+    case 6: return launch_one<STATS, 1, 4, 1, 5>(P, stream);
+    case 7: return launch_one<STATS, 1, 4, 0, 5>(P, stream);
+    case 8: return launch_one<STATS, 2, 8, 1, 5>(P, stream);
     case 9: return launch_sched<STATS, 1, 32, 16>(P, stream);
-    default: return launch_one<STATS, 0, 4, true, 1>(P, stream);
+    case 10: return launch_one<STATS, 2, 16, 1, 5>(P, stream);
+    case 11: return launch_one<STATS, 1, 8, 1, 5>(P, stream);
+    case 12: return launch_one<STATS, 1, 4, 1, 6>(P, stream);
+    case 13: return launch_one<STATS, 1, 4, 1, 7>(P, stream);
+    case 14: return launch_one<STATS, 1, 4, 1, 8>(P, stream);
+    case 15: return launch_one<STATS, 0, 4, 1, 6>(P, stream);
+    case 16: return launch_one<STATS, 1, 4, 32, 6>(P, stream);
+    case 17: return launch_one<STATS, 1, 4, 48, 6>(P, stream);
+    case 18: return launch_one<STATS, 1, 4, 16, 6>(P, stream);
+    default: return launch_one<STATS, 0, 4, 1, 1>(P, stream);
     }
 }
 
@@ -1254,6 +1336,10 @@ static int render_impl(pt_context* ctx, const pt_camera* cam, uint32_t spp, uint
         stats->wave_hits = h[8];
         stats->wave_sky = h[9];
         stats->wave_segments = h[10];
+        stats->cycles_node_walk = h[11];
+        stats->cycles_leaf_tests = h[12];
+        stats->cycles_shading = h[13];
+        stats->cycles_total = h[14];
     }
     return PT_OK;
 }
@@ -1338,7 +1424,7 @@ PT_API uint32_t pt_local_rows(const pt_context* ctx) { return ctx ? ctx->rows : 
 
 PT_API int pt_set_kernel_variant(pt_context* ctx, int variant)
 {
-    if (!ctx || variant < 0 || variant > 9) return PT_ERR_ARG;
+    if (!ctx || variant < 0 || variant > 18) return PT_ERR_ARG;
     ctx->variant = variant;
     return PT_OK;
 }

@@ -67,7 +67,7 @@ def test_render_bitexact(gpu_available, scenes, name, W, H, spp, chunks):
     assert pt.frames == ref.frames == chunks
 
 
-@pytest.mark.parametrize("variant", range(1, 10))
+@pytest.mark.parametrize("variant", range(1, 19))
 def test_every_kernel_variant_bitexact(gpu_available, scenes, variant):
     # all trace-kernel variants (schedules, LDS staging, occupancy) produce the reference's bits
     pt, cam, ref, osc = pair(scenes / "test_shapes.scene.json", 72, 40)

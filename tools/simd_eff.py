@@ -26,5 +26,8 @@ for v in [int(x) for x in a.variants.split(",")]:
         ("hit_shade", "hits", "wave_hits"), ("sky", "sky_lookups", "wave_sky"), ("segment", "segments", "wave_segments")]}
     per_sample = {k: round(st[k] / st["samples"], 3) for k in ("node_tests", "prim_tests", "hits", "sky_lookups", "segments",
                                                                 "wave_node_iters", "wave_prim_iters", "wave_hits", "wave_sky", "wave_segments")}
-    res[v] = {"simd_efficiency": eff, "per_sample": per_sample}
+    tot = st["cycles_total"] or 1
+    shares = {k: round(st[k] / tot, 3) for k in ("cycles_node_walk", "cycles_leaf_tests", "cycles_shading")}
+    res[v] = {"simd_efficiency": eff, "per_sample": per_sample, "cycle_share": shares,
+              "wave_cycles_per_sample": round(tot / st["samples"] * 64, 1)}
 print(json.dumps({"scene": pathlib.Path(a.scene).name, "variants": res}, indent=1))
