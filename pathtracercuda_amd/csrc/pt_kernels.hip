@@ -57,6 +57,9 @@ struct TraceParams {
     uint32_t spp, chunks, ignoreFirst;
     uint32_t tilesX, tilesY;
     uint32_t nodeCount, primCount, stackDepth, slabFast;
+    const float4* cnodes;       // child-box records (4 per interior node), see traverse_cb
+    uint32_t cnodeCount, rootWord;
+    float rootBox[6];           // (min.x, max.x, min.y, max.y, min.z, max.z) of the root
     DevCamera cam;
 };
 
@@ -387,54 +390,135 @@ PT_DEV uint32_t traverse(const float4* __restrict__ nodes, const float4* __restr
                 else cur = stack[64u * (--sp)];
             }
         }
-    } else {
-        // threshold while-while: leave the interior walk as soon as WW lanes have a leaf pending
-        uint32_t leafOff = 0, leafCnt = 0;
-        bool done = false;
-        while (!done) {
-            for (;;) {
-                const bool walking = leafCnt == 0;
-                const unsigned long long mw = __ballot(walking);
-                const unsigned long long ml = __ballot(!walking);
-                if (mw == 0ull || __popcll(ml) >= WW) break;
-                if (walking) {
-                    if (STATS) { cnt.node_tests++; wave_tick(cnt.w_node); }
-                    const NodeHit nh = test(cur);
-                    const uint32_t count = nh.pca >> 16;
-                    const bool isNeg = (negMask >> ((nh.pca >> 8) & 0xffu)) & 1u;
-                    const uint32_t nearC = isNeg ? nh.offset : cur + 1;
-                    const uint32_t farC = isNeg ? cur + 1 : nh.offset;
-                    if (nh.hit) {
-                        if (count > 0) {
-                            leafOff = nh.offset;
-                            leafCnt = count;
-                        } else {
-                            stack[64u * sp] = farC;
-                            ++sp;
-                            cur = nearC;
-                        }
-                    } else {
-                        if (sp == 0) { done = true; break; }
-                        cur = stack[64u * (--sp)];
-                    }
+    }
+    tHit = tMax;
+    return elem;
+}
+
+// ---------------------------------------------------------------------------------------------
+// Child-box traversal (WW == 3).  Device layout "cnodes": one 64-byte record per INTERIOR node of
+// the reference BVH holding both children's boxes and references:
+//   Q0 = (L.min.x, L.max.x, L.min.y, L.max.y)   Q1 = (L.min.z, L.max.z, R.min.z, R.max.z)
+//   Q2 = (R.min.x, R.max.x, R.min.y, R.max.y)   Q3 = (L word, R word, split axis, 0)
+// L = first child (node + 1), R = second child (node.offset); a child word is (count << 24 | prim
+// offset) for a leaf and the child's record index for an interior node.
+//
+// Why it is exact: the slab test of AABB.inl:22-44 (node_test) starts its running upper bound at
+// the ray's t_max and every update is a min that skips NaN, so for any ray
+//     hit(t_max) = (X > lo) && (t_max > lo)
+// with lo and X (the same test started from +inf) independent of t_max.  hitBVH tests a node's
+// near child right after the node (t_max unchanged) and its far child when it is popped, after
+// the near subtree may have lowered t_max.  Here both children are tested when their parent is
+// visited; the far child is pushed with its lo and, when popped, re-tested as t_max > lo with the
+// then-current t_max -- the reference's verdict.  Visit order, node tests and primitive tests per
+// lane are unchanged; a visit costs one dependent fetch instead of two, and leaves cost none.
+// ---------------------------------------------------------------------------------------------
+struct SlabRay {
+    f2v ox2, oy2, oz2, ix2, iy2, iz2;
+    f3 o;
+    float ix, iy, iz;
+    bool fast;
+};
+
+// lo and X of one box (see above); the fast form under the same conditions as node_test_fast.
+PT_DEV float slab_lo_x(const SlabRay& R, f2v bx, f2v by, f2v bz, float tMin, float& X)
+{
+    if (R.fast) {
+        const f2v tx = (bx - R.ox2) * R.ix2;
+        const f2v ty = (by - R.oy2) * R.iy2;
+        const f2v tz = (bz - R.oz2) * R.iz2;
+        X = __builtin_fminf(__builtin_fmaxf(tx.x, tx.y), __builtin_fminf(__builtin_fmaxf(ty.x, ty.y), __builtin_fmaxf(tz.x, tz.y)));
+        return __builtin_fmaxf(__builtin_fmaxf(tMin, __builtin_fminf(tx.x, tx.y)),
+                               __builtin_fmaxf(__builtin_fminf(ty.x, ty.y), __builtin_fminf(tz.x, tz.y)));
+    }
+    float lo = tMin, hi = __builtin_inff();
+    const float inv[3] = {R.ix, R.iy, R.iz};
+    const float org[3] = {R.o.x, R.o.y, R.o.z};
+    const f2v b[3] = {bx, by, bz};
+#pragma unroll
+    for (int k = 0; k < 3; ++k) {
+        float t0 = (b[k].x - org[k]) * inv[k], t1 = (b[k].y - org[k]) * inv[k];
+        if (inv[k] < 0.0f) { const float tmp = t0; t0 = t1; t1 = tmp; }
+        lo = t0 > lo ? t0 : lo;
+        hi = t1 < hi ? t1 : hi;
+    }
+    X = hi;
+    return lo;
+}
+
+template <bool STATS>
+PT_DEV uint32_t traverse_cb(const float4* __restrict__ cnodes, const float4* __restrict__ prims, uint2* stack,
+                            const TraceParams& P, f3 o, f3 d, float& tHit, Counters& cnt)
+{
+    const float tMin = 0.001f;
+    float tMax = kFltMax;
+    SlabRay R;
+    R.o = o;
+    R.ix = 1.0f / d.x;
+    R.iy = 1.0f / d.y;
+    R.iz = 1.0f / d.z;
+    R.fast = P.slabFast && __builtin_isfinite(R.ix) && __builtin_isfinite(R.iy) && __builtin_isfinite(R.iz);
+    R.ox2 = f2(o.x, o.x);
+    R.oy2 = f2(o.y, o.y);
+    R.oz2 = f2(o.z, o.z);
+    R.ix2 = f2(R.ix, R.ix);
+    R.iy2 = f2(R.iy, R.iy);
+    R.iz2 = f2(R.iz, R.iz);
+    const uint32_t negMask = (d.x < 0.0f ? 1u : 0u) | (d.y < 0.0f ? 2u : 0u) | (d.z < 0.0f ? 4u : 0u);
+    uint32_t sp = 0, elem = 0xffffffffu, cur = P.rootWord;
+    // pops the next pending far child that still passes its box test under the current t_max
+    auto pop = [&]() -> bool {
+        while (sp > 0) {
+            const uint2 e = stack[64u * (--sp)];
+            if (tMax > __uint_as_float(e.y)) { cur = e.x; return true; }
+        }
+        return false;
+    };
+    if (STATS) { cnt.node_tests++; wave_tick(cnt.w_node); }
+    float X;
+    const float lo0 = slab_lo_x(R, f2(P.rootBox[0], P.rootBox[1]), f2(P.rootBox[2], P.rootBox[3]),
+                                f2(P.rootBox[4], P.rootBox[5]), tMin, X);
+    bool done = !(X > lo0 && tMax > lo0);
+    while (!done) {
+        while ((cur >> 24) == 0u) {                               // interior walk
+            if (STATS) { cnt.node_tests += 2; wave_tick(cnt.w_node); }
+            const float4 Q0 = cnodes[4 * cur], Q1 = cnodes[4 * cur + 1];
+            const float4 Q2 = cnodes[4 * cur + 2], Q3 = cnodes[4 * cur + 3];
+            float XL, XR;
+            const float loL = slab_lo_x(R, f2(Q0.x, Q0.y), f2(Q0.z, Q0.w), f2(Q1.x, Q1.y), tMin, XL);
+            const float loR = slab_lo_x(R, f2(Q2.x, Q2.y), f2(Q2.z, Q2.w), f2(Q1.z, Q1.w), tMin, XR);
+            const bool hL = XL > loL && tMax > loL, hR = XR > loR && tMax > loR;
+            const bool isNeg = (negMask >> __float_as_uint(Q3.z)) & 1u;    // trace.cu:66-77
+            const uint32_t wL = __float_as_uint(Q3.x), wR = __float_as_uint(Q3.y);
+            const bool hN = isNeg ? hR : hL, hF = isNeg ? hL : hR;
+            const uint32_t wN = isNeg ? wR : wL, wF = isNeg ? wL : wR;
+            const float loF = isNeg ? loL : loR;
+            if (hN) {
+                if (hF) {
+                    stack[64u * sp] = make_uint2(wF, __float_as_uint(loF));
+                    ++sp;
                 }
-            }
-            if (done) break;
-            if (leafCnt > 0) {
-                while (leafCnt > 0) {
-                    if (STATS) { cnt.prim_tests++; wave_tick(cnt.w_prim); }
-                    float t;
-                    if (prim_hit(prims, leafOff, o, d, tMin, tMax, t)) {
-                        tMax = t;
-                        elem = leafOff;
-                    }
-                    ++leafOff;
-                    --leafCnt;
-                }
-                if (sp == 0) done = true;
-                else cur = stack[64u * (--sp)];
+                cur = wN;
+            } else if (hF) {
+                cur = wF;
+            } else if (!pop()) {
+                done = true;
+                break;
             }
         }
+        if (done) break;
+        uint32_t leafOff = cur & 0xffffffu, leafCnt = cur >> 24;  // in-order leaf tests
+        while (leafCnt > 0) {
+            if (STATS) { cnt.prim_tests++; wave_tick(cnt.w_prim); }
+            float t;
+            if (prim_hit(prims, leafOff, o, d, tMin, tMax, t)) {
+                tMax = t;
+                elem = leafOff;
+            }
+            ++leafOff;
+            --leafCnt;
+        }
+        if (!pop()) done = true;
     }
     tHit = tMax;
     return elem;
@@ -795,16 +879,20 @@ __global__ void __launch_bounds__(WPB * 64, MINW) trace_kernel(TraceParams P)
     extern __shared__ float4 lds4[];
     const uint32_t lane = threadIdx.x & 63u;
     const uint32_t wave = threadIdx.x >> 6;
-    const uint32_t sceneF4 = (SL >= 1 ? 2u * P.nodeCount : 0u) + (SL >= 2 ? 4u * P.primCount : 0u);
+    const float4* gnodes = WW == 3 ? P.cnodes : P.nodes;
+    const uint32_t nodeF4 = WW == 3 ? 4u * P.cnodeCount : 2u * P.nodeCount;
+    const uint32_t sceneF4 = (SL >= 1 ? nodeF4 : 0u) + (SL >= 2 ? 4u * P.primCount : 0u);
     if (SL >= 1) {
-        for (uint32_t i = threadIdx.x; i < 2u * P.nodeCount; i += WPB * 64) lds4[i] = P.nodes[i];
+        for (uint32_t i = threadIdx.x; i < nodeF4; i += WPB * 64) lds4[i] = gnodes[i];
         if (SL >= 2)
-            for (uint32_t i = threadIdx.x; i < 4u * P.primCount; i += WPB * 64) lds4[2u * P.nodeCount + i] = P.prims[i];
+            for (uint32_t i = threadIdx.x; i < 4u * P.primCount; i += WPB * 64) lds4[nodeF4 + i] = P.prims[i];
         __syncthreads();
     }
-    const float4* __restrict__ nodes = SL >= 1 ? lds4 : P.nodes;
-    const float4* __restrict__ prims = SL >= 2 ? lds4 + 2u * P.nodeCount : P.prims;
-    uint32_t* stack = reinterpret_cast<uint32_t*>(lds4 + sceneF4) + wave * P.stackDepth * 64u + lane;
+    const float4* __restrict__ nodes = SL >= 1 ? lds4 : gnodes;
+    const float4* __restrict__ prims = SL >= 2 ? lds4 + nodeF4 : P.prims;
+    // wave stacks: stackDepth x 64 entries of u32 (node index), or of uint2 (word, lo) for WW == 3
+    uint32_t* stack = reinterpret_cast<uint32_t*>(lds4 + sceneF4) + (WW == 3 ? 2u : 1u) * wave * P.stackDepth * 64u +
+                      (WW == 3 ? 2u : 1u) * lane;
     const PixelCtx pc = pixel_of(P, blockIdx.x * (uint32_t)WPB + wave, lane);
     Counters cnt = {};
     if (pc.valid) {
@@ -817,7 +905,8 @@ __global__ void __launch_bounds__(WPB * 64, MINW) trace_kernel(TraceParams P)
         while (ps.alive) {
             if (STATS) { cnt.segments++; wave_tick(cnt.w_segments); }
             float t;
-            const uint32_t e = traverse<STATS, WW>(nodes, prims, stack, ps.o, ps.d, P.slabFast != 0, t, cnt);
+            const uint32_t e = WW == 3 ? traverse_cb<STATS>(nodes, prims, reinterpret_cast<uint2*>(stack), P, ps.o, ps.d, t, cnt)
+                                       : traverse<STATS, WW>(nodes, prims, stack, ps.o, ps.d, P.slabFast != 0, t, cnt);
             uint64_t tS = STATS ? __builtin_amdgcn_s_memtime() : 0;
             if (shade<STATS>(P, prims, e, t, ps, rng, cnt)) finish_path<STATS>(P, ps, rng, fx, fy, cnt);
             if (STATS) wave_time(cnt.cyc_shade, tS);
@@ -986,6 +1075,9 @@ struct pt_context {
     float4* nodes = nullptr;
     float4* prims = nullptr;
     float4* mats = nullptr;
+    float4* cnodes = nullptr;   // child-box records (traverse_cb); null when the scene exceeds its encoding
+    uint32_t cnodeCount = 0, rootWord = 0;
+    float rootBox[6] = {};
     uint32_t nodeCount = 0, primCount = 0, stackDepth = 1;
     bool slabFast = true;
     int variant = 0;
@@ -1029,8 +1121,10 @@ static int fail(pt_context* ctx, int code, const char* msg)
 template <bool STATS, int SL, int WPB, int WW, int MINW>
 static hipError_t launch_one(const TraceParams& P, hipStream_t stream)
 {
-    const size_t sceneBytes = ((SL >= 1 ? 2 * (size_t)P.nodeCount : 0) + (SL >= 2 ? 4 * (size_t)P.primCount : 0)) * sizeof(float4);
-    const size_t lds = sceneBytes + (size_t)WPB * P.stackDepth * 64 * sizeof(uint32_t);
+    const size_t nodeF4 = WW == 3 ? 4 * (size_t)P.cnodeCount : 2 * (size_t)P.nodeCount;
+    const size_t sceneBytes = ((SL >= 1 ? nodeF4 : 0) + (SL >= 2 ? 4 * (size_t)P.primCount : 0)) * sizeof(float4);
+    const size_t lds = sceneBytes + (size_t)WPB * P.stackDepth * 64 * (WW == 3 ? 8 : 4);
+    if (WW == 3 && P.cnodes == nullptr) return launch_one<STATS, SL, WPB, 1, MINW>(P, stream);  // no child-box layout
     if (lds > 160 * 1024) return hipErrorInvalidValue;
     static bool attrSet = false;
     if (!attrSet) {
@@ -1074,9 +1168,11 @@ static hipError_t launch_variant(int v, const TraceParams& P, hipStream_t stream
     case 13: return launch_one<STATS, 1, 4, 1, 7>(P, stream);
     case 14: return launch_one<STATS, 1, 4, 1, 8>(P, stream);
     case 15: return launch_one<STATS, 0, 4, 1, 6>(P, stream);
-    case 16: return launch_one<STATS, 1, 4, 32, 6>(P, stream);
-    case 17: return launch_one<STATS, 1, 4, 48, 6>(P, stream);
-    case 18: return launch_one<STATS, 1, 4, 16, 6>(P, stream);
+    case 16: return launch_one<STATS, 1, 4, 3, 6>(P, stream);
+    case 17: return launch_one<STATS, 0, 4, 3, 6>(P, stream);
+    case 18: return launch_one<STATS, 1, 8, 3, 6>(P, stream);
+    case 19: return launch_one<STATS, 1, 4, 3, 5>(P, stream);
+    case 20: return launch_one<STATS, 0, 4, 3, 5>(P, stream);
     default: return launch_one<STATS, 0, 4, 1, 1>(P, stream);
     }
 }
@@ -1084,9 +1180,13 @@ static hipError_t launch_variant(int v, const TraceParams& P, hipStream_t stream
 static int pick_variant(const pt_context* ctx)
 {
     if (ctx->variant > 0) return ctx->variant;
-    // measured on MI355X (tools/ab_variants.py, profiles/): staging the BVH nodes in LDS cuts the
-    // latency of the dependent node fetches; while-while traversal + 5 waves/SIMD win on the
-    // 484-object scene.  Large BVHs (e.g. the 100k-object stress scene) stay in global memory.
+    // measured on MI355X (tools/ab_variants.py, profiles/): child-box traversal (one dependent
+    // fetch per interior visit, leaves inline) with while-while leaf batching and 5 waves/SIMD
+    // wins on every scene; the child-box records are staged in LDS when they fit in 48 KB
+    // (cornell, the 484-object scene) and read through the caches otherwise (100k objects).
+    // Scenes outside the child-box encoding fall back to the node-at-a-time walk (launch_one).
+    const size_t cbBytes = 4 * (size_t)ctx->cnodeCount * sizeof(float4);
+    if (ctx->cnodes) return cbBytes <= 48 * 1024 ? 19 : 20;
     const size_t nodeBytes = 2 * (size_t)ctx->nodeCount * sizeof(float4);
     return nodeBytes <= 48 * 1024 ? 6 : 4;
 }
@@ -1150,6 +1250,7 @@ PT_API void pt_destroy(pt_context* ctx)
     (void)hipFree(ctx->nodes);
     (void)hipFree(ctx->prims);
     (void)hipFree(ctx->mats);
+    (void)hipFree(ctx->cnodes);
     (void)hipFree(ctx->texTable);
     (void)hipFree(ctx->stats);
     for (auto& t : ctx->hostTex) (void)hipFree((void*)t.texels);
@@ -1212,6 +1313,31 @@ PT_API int pt_set_scene(pt_context* ctx, const pt_bvh_node* nodes, uint32_t node
         for (int k = 0; k < 3; ++k)   // the fast slab test needs ordered, non-NaN bounds
             if (!(n.aabb_min[k] <= n.aabb_max[k])) slabFast = false;
     }
+    // child-box records: interior nodes renumbered in order; a child word is (count << 24 | prim
+    // offset) for a leaf, the record index otherwise (needs counts < 256 and offsets < 2^24)
+    std::vector<uint32_t> rec(node_count, 0xffffffffu);
+    uint32_t interior = 0;
+    bool cbOk = node_count < (1u << 24) && prim_count < (1u << 24);
+    for (uint32_t i = 0; i < node_count; ++i) {
+        const uint32_t count = nodes[i].primitive_count_axis >> 16;
+        if (count == 0) rec[i] = interior++;
+        else if (count > 255) cbOk = false;
+    }
+    auto word = [&](uint32_t i) {
+        const uint32_t count = nodes[i].primitive_count_axis >> 16;
+        return count ? (count << 24) | nodes[i].offset : rec[i];
+    };
+    std::vector<float4> hc(4 * (size_t)std::max(interior, 1u), make_float4(0.0f, 0.0f, 0.0f, 0.0f));
+    for (uint32_t i = 0; cbOk && i < node_count; ++i) {
+        if (rec[i] == 0xffffffffu) continue;
+        const pt_bvh_node& L = nodes[i + 1];
+        const pt_bvh_node& R = nodes[nodes[i].offset];
+        float4* q = &hc[4 * (size_t)rec[i]];
+        q[0] = make_float4(L.aabb_min[0], L.aabb_max[0], L.aabb_min[1], L.aabb_max[1]);
+        q[1] = make_float4(L.aabb_min[2], L.aabb_max[2], R.aabb_min[2], R.aabb_max[2]);
+        q[2] = make_float4(R.aabb_min[0], R.aabb_max[0], R.aabb_min[1], R.aabb_max[1]);
+        q[3] = make_float4(u2f(word(i + 1)), u2f(word(nodes[i].offset)), u2f((nodes[i].primitive_count_axis >> 8) & 0xffu), 0.0f);
+    }
     for (uint32_t i = 0; i < prim_count; ++i) {
         const pt_hittable& h = prims[i];
         const float(&R)[3][4] = h.inv_transform_rows;
@@ -1228,14 +1354,25 @@ PT_API int pt_set_scene(pt_context* ctx, const pt_bvh_node* nodes, uint32_t node
     (void)hipFree(ctx->nodes);
     (void)hipFree(ctx->prims);
     (void)hipFree(ctx->mats);
-    ctx->nodes = ctx->prims = ctx->mats = nullptr;
-    ctx->nodeCount = ctx->primCount = 0;
+    (void)hipFree(ctx->cnodes);
+    ctx->nodes = ctx->prims = ctx->mats = ctx->cnodes = nullptr;
+    ctx->nodeCount = ctx->primCount = ctx->cnodeCount = 0;
     PT_HIP_CHECK(ctx, hipMalloc(&ctx->nodes, hn.size() * sizeof(float4)));
     PT_HIP_CHECK(ctx, hipMalloc(&ctx->prims, hp.size() * sizeof(float4)));
     PT_HIP_CHECK(ctx, hipMalloc(&ctx->mats, hm.size() * sizeof(float4)));
     PT_HIP_CHECK(ctx, hipMemcpy(ctx->nodes, hn.data(), hn.size() * sizeof(float4), hipMemcpyHostToDevice));
     PT_HIP_CHECK(ctx, hipMemcpy(ctx->prims, hp.data(), hp.size() * sizeof(float4), hipMemcpyHostToDevice));
     PT_HIP_CHECK(ctx, hipMemcpy(ctx->mats, hm.data(), hm.size() * sizeof(float4), hipMemcpyHostToDevice));
+    if (cbOk) {
+        PT_HIP_CHECK(ctx, hipMalloc(&ctx->cnodes, hc.size() * sizeof(float4)));
+        PT_HIP_CHECK(ctx, hipMemcpy(ctx->cnodes, hc.data(), hc.size() * sizeof(float4), hipMemcpyHostToDevice));
+        ctx->cnodeCount = interior;
+    }
+    ctx->rootWord = word(0);
+    for (int k = 0; k < 3; ++k) {
+        ctx->rootBox[2 * k] = nodes[0].aabb_min[k];
+        ctx->rootBox[2 * k + 1] = nodes[0].aabb_max[k];
+    }
     ctx->nodeCount = node_count;
     ctx->primCount = prim_count;
     ctx->slabFast = slabFast;
@@ -1312,6 +1449,10 @@ static int render_impl(pt_context* ctx, const pt_camera* cam, uint32_t spp, uint
     P.primCount = ctx->primCount;
     P.stackDepth = ctx->stackDepth;
     P.slabFast = ctx->slabFast ? 1u : 0u;
+    P.cnodes = ctx->cnodes;
+    P.cnodeCount = ctx->cnodeCount;
+    P.rootWord = ctx->rootWord;
+    for (int k = 0; k < 6; ++k) P.rootBox[k] = ctx->rootBox[k];
     if (stats) PT_HIP_CHECK(ctx, hipMemsetAsync(ctx->stats, 0, 16 * sizeof(unsigned long long), ctx->stream));
     PT_HIP_CHECK(ctx, hipEventRecord(ctx->ev0, ctx->stream));
     const int variant = pick_variant(ctx);
@@ -1424,7 +1565,7 @@ PT_API uint32_t pt_local_rows(const pt_context* ctx) { return ctx ? ctx->rows : 
 
 PT_API int pt_set_kernel_variant(pt_context* ctx, int variant)
 {
-    if (!ctx || variant < 0 || variant > 18) return PT_ERR_ARG;
+    if (!ctx || variant < 0 || variant > 20) return PT_ERR_ARG;
     ctx->variant = variant;
     return PT_OK;
 }

@@ -67,7 +67,7 @@ def test_render_bitexact(gpu_available, scenes, name, W, H, spp, chunks):
     assert pt.frames == ref.frames == chunks
 
 
-@pytest.mark.parametrize("variant", range(1, 19))
+@pytest.mark.parametrize("variant", range(1, 21))
 def test_every_kernel_variant_bitexact(gpu_available, scenes, variant):
     # all trace-kernel variants (schedules, LDS staging, occupancy) produce the reference's bits
     pt, cam, ref, osc = pair(scenes / "test_shapes.scene.json", 72, 40)
@@ -76,6 +76,33 @@ def test_every_kernel_variant_bitexact(gpu_available, scenes, variant):
     ref.render(osc.camera, 4, True, chunks=2)
     assert_bitexact(pt.accum(), ref.accum, f"variant {variant}")
     assert np.array_equal(pt.rng_state(), ref.rng_array())
+
+
+@pytest.mark.parametrize("nprims", [484, 200])
+def test_single_leaf_bvh_every_traversal(gpu_available, scenes, nprims):
+    # a caller-supplied BVH through pt_set_scene: the root is one leaf of nprims primitives.  484 is
+    # beyond the child-box encoding (leaf counts < 256), so those variants fall back; 200 runs the
+    # child-box traversal with a leaf root.  Results must still be the reference's.
+    import ctypes as C
+    from pathtracercuda_amd import _native as N
+    W, H = 48, 32
+    pt, cam, ref, osc = pair(scenes / "generated_scene.scene.json", W, H)
+    root = po.BVHNode.from_buffer_copy(bytes(osc.nodes[0]))
+    root.offset = 0
+    root.primitiveCountAxis = nprims << 16
+    osc.nodes = (po.BVHNode * 1)(root)
+    osc.node_count = 1
+    osc.prim_count = nprims
+    nodes = (pa.PtBvhNode * 1).from_buffer_copy(bytes(osc.nodes))
+    prims = (pa.PtHittable * nprims).from_buffer_copy(bytes(osc.prims)[:nprims * C.sizeof(pa.PtHittable)])
+    N.check_ctx(N.hip().pt_set_scene(pt._ctx, nodes, 1, prims, nprims), pt._ctx)
+    ref.render(osc.camera, 2, True, chunks=1)
+    for variant in (0, 6, 12, 16, 17, 20):
+        st = pt.rng_state()
+        pt.set_kernel_variant(variant)
+        pt.render_raw(cam, 2, 1, True)
+        assert_bitexact(pt.accum(), ref.accum, f"single leaf {nprims}, variant {variant}")
+        pt.set_rng_state(st)
 
 
 def test_history_semantics(gpu_available, scenes):
