@@ -154,10 +154,15 @@ PT_API int pt_write_rng(pt_context *ctx, const uint32_t *src);
 
 PT_API uint32_t pt_local_rows(const pt_context *ctx);
 
-/* Tuning knob for A/B measurements: 0 = automatic (default); 1..20 select a trace-kernel variant
+/* Tuning knob for A/B measurements: 0 = automatic (default); 1..22 select a trace-kernel variant
  * (workgroup size, BVH/primitives staged in LDS or read through the caches, traversal loop shape,
  * occupancy target).  All variants produce bit-identical results. */
 PT_API int pt_set_kernel_variant(pt_context *ctx, int variant);
+
+/* Tile dispatch order: 0 = by the measured cost of each 8x8 tile, most expensive first (default;
+ * the first launch after a scene, texture or camera change records the costs in row-major
+ * order), 1 = always row-major.  Results are identical; only the launch tail changes. */
+PT_API int pt_set_schedule(pt_context *ctx, int mode);
 PT_API const char *pt_last_error(const pt_context *ctx);
 
 #ifdef __cplusplus

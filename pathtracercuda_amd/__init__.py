@@ -211,6 +211,10 @@ class Pathtracer:
     def set_kernel_variant(self, variant: int) -> None:
         N.check_ctx(N.hip().pt_set_kernel_variant(self._ctx, int(variant)), self._ctx)
 
+    def set_schedule(self, mode: int) -> None:
+        """0 = cost-sorted tile dispatch (default), 1 = row-major (pt_set_schedule)."""
+        N.check_ctx(N.hip().pt_set_schedule(self._ctx, int(mode)), self._ctx)
+
     def copy_accum_to_device(self, dst_ptr: int, nbytes: int) -> None:
         N.check_ctx(N.hip().pt_copy_accum_device(self._ctx, C.c_void_p(int(dst_ptr)), int(nbytes)), self._ctx)
 

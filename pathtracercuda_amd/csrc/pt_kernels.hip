@@ -60,6 +60,8 @@ struct TraceParams {
     const float4* cnodes;       // child-box records (4 per interior node), see traverse_cb
     uint32_t cnodeCount, rootWord;
     float rootBox[6];           // (min.x, max.x, min.y, max.y, min.z, max.z) of the root
+    const uint32_t* order;      // tile dispatch order (null: row-major), see "Tile scheduling"
+    uint32_t* tileCost;         // per-tile shader-clock cycles of this launch (null: not recorded)
     DevCamera cam;
 };
 
@@ -479,6 +481,7 @@ PT_DEV uint32_t traverse_cb(const float4* __restrict__ cnodes, const float4* __r
     const float lo0 = slab_lo_x(R, f2(P.rootBox[0], P.rootBox[1]), f2(P.rootBox[2], P.rootBox[3]),
                                 f2(P.rootBox[4], P.rootBox[5]), tMin, X);
     bool done = !(X > lo0 && tMax > lo0);
+    uint64_t tPhase = STATS ? __builtin_amdgcn_s_memtime() : 0;
     while (!done) {
         while ((cur >> 24) == 0u) {                               // interior walk
             if (STATS) { cnt.node_tests += 2; wave_tick(cnt.w_node); }
@@ -506,6 +509,7 @@ PT_DEV uint32_t traverse_cb(const float4* __restrict__ cnodes, const float4* __r
                 break;
             }
         }
+        if (STATS) wave_time(cnt.cyc_node, tPhase);
         if (done) break;
         uint32_t leafOff = cur & 0xffffffu, leafCnt = cur >> 24;  // in-order leaf tests
         while (leafCnt > 0) {
@@ -518,7 +522,122 @@ PT_DEV uint32_t traverse_cb(const float4* __restrict__ cnodes, const float4* __r
             ++leafOff;
             --leafCnt;
         }
+        if (STATS) wave_time(cnt.cyc_leaf, tPhase);
         if (!pop()) done = true;
+    }
+    tHit = tMax;
+    return elem;
+}
+
+// ---------------------------------------------------------------------------------------------
+// Speculative child-box traversal (WW == 5).  While some lane of the wave still searches for its
+// next leaf, lanes that already hold one keep walking and queue a second leaf (Aila & Laine's
+// speculative traversal).  Exactness: child boxes are nested (a parent's bounds are the union of
+// its children's), so with the same ray the rounded slab values satisfy lo_child >= lo_parent;
+// walking with a stale (larger) t_max therefore visits a superset of the reference's nodes, in
+// the reference's order (near/far depend on the ray only), and finds a superset of its leaves in
+// order.  Leaves are tested strictly in that order and each is re-checked as t_max > lo with the
+// t_max of that moment -- exactly the reference's verdict for the leaf (an ancestor culled by the
+// reference has lo_anc <= lo_leaf, so the leaf fails the check too).  Per-lane node culling,
+// primitive tests and tie rules are the reference's; speculative node tests are extra work only.
+// ---------------------------------------------------------------------------------------------
+template <bool STATS>
+PT_DEV uint32_t traverse_spec(const float4* __restrict__ cnodes, const float4* __restrict__ prims, uint2* stack,
+                              const TraceParams& P, f3 o, f3 d, float& tHit, Counters& cnt)
+{
+    const float tMin = 0.001f;
+    float tMax = kFltMax;
+    SlabRay R;
+    R.o = o;
+    R.ix = 1.0f / d.x;
+    R.iy = 1.0f / d.y;
+    R.iz = 1.0f / d.z;
+    R.fast = P.slabFast && __builtin_isfinite(R.ix) && __builtin_isfinite(R.iy) && __builtin_isfinite(R.iz);
+    R.ox2 = f2(o.x, o.x);
+    R.oy2 = f2(o.y, o.y);
+    R.oz2 = f2(o.z, o.z);
+    R.ix2 = f2(R.ix, R.ix);
+    R.iy2 = f2(R.iy, R.iy);
+    R.iz2 = f2(R.iz, R.iz);
+    const uint32_t negMask = (d.x < 0.0f ? 1u : 0u) | (d.y < 0.0f ? 2u : 0u) | (d.z < 0.0f ? 4u : 0u);
+    uint32_t sp = 0, elem = 0xffffffffu;
+    uint32_t cur = P.rootWord;
+    float curLo;
+    // leaf queue (FIFO, capacity 2): words and lo values
+    uint32_t qw0 = 0, qw1 = 0, qn = 0;
+    float ql0 = 0.0f, ql1 = 0.0f;
+    if (STATS) { cnt.node_tests++; wave_tick(cnt.w_node); }
+    float X;
+    curLo = slab_lo_x(R, f2(P.rootBox[0], P.rootBox[1]), f2(P.rootBox[2], P.rootBox[3]), f2(P.rootBox[4], P.rootBox[5]),
+                      tMin, X);
+    bool done = !(X > curLo && tMax > curLo);
+    uint64_t tPhase = STATS ? __builtin_amdgcn_s_memtime() : 0;
+    for (;;) {
+        // walk until every lane that can still walk holds a leaf; lanes holding one queue a second
+        for (;;) {
+            if (__ballot(!done && qn == 0) == 0ull) break;
+            if (!done && qn < 2u) {
+                if (cur >> 24) {                                   // leaf: queue it, pop the next
+                    if (qn == 0u) { qw0 = cur; ql0 = curLo; }
+                    else { qw1 = cur; ql1 = curLo; }
+                    ++qn;
+                    done = true;
+                    while (sp > 0) {
+                        const uint2 e = stack[64u * (--sp)];
+                        if (tMax > __uint_as_float(e.y)) { cur = e.x; curLo = __uint_as_float(e.y); done = false; break; }
+                    }
+                } else {
+                    if (STATS) { cnt.node_tests += 2; wave_tick(cnt.w_node); }
+                    const float4 Q0 = cnodes[4 * cur], Q1 = cnodes[4 * cur + 1];
+                    const float4 Q2 = cnodes[4 * cur + 2], Q3 = cnodes[4 * cur + 3];
+                    float XL, XR;
+                    const float loL = slab_lo_x(R, f2(Q0.x, Q0.y), f2(Q0.z, Q0.w), f2(Q1.x, Q1.y), tMin, XL);
+                    const float loR = slab_lo_x(R, f2(Q2.x, Q2.y), f2(Q2.z, Q2.w), f2(Q1.z, Q1.w), tMin, XR);
+                    const bool hL = XL > loL && tMax > loL, hR = XR > loR && tMax > loR;
+                    const bool isNeg = (negMask >> __float_as_uint(Q3.z)) & 1u;
+                    const uint32_t wL = __float_as_uint(Q3.x), wR = __float_as_uint(Q3.y);
+                    const bool hN = isNeg ? hR : hL, hF = isNeg ? hL : hR;
+                    const uint32_t wN = isNeg ? wR : wL, wF = isNeg ? wL : wR;
+                    const float loN = isNeg ? loR : loL, loF = isNeg ? loL : loR;
+                    if (hN && hF) {
+                        stack[64u * sp] = make_uint2(wF, __float_as_uint(loF));
+                        ++sp;
+                    }
+                    if (hN || hF) {
+                        cur = hN ? wN : wF;
+                        curLo = hN ? loN : loF;
+                    } else {
+                        done = true;
+                        while (sp > 0) {
+                            const uint2 e = stack[64u * (--sp)];
+                            if (tMax > __uint_as_float(e.y)) { cur = e.x; curLo = __uint_as_float(e.y); done = false; break; }
+                        }
+                    }
+                }
+            }
+        }
+        if (STATS) wave_time(cnt.cyc_node, tPhase);
+        if (qn == 0u) break;                                       // done and nothing queued
+        // oldest queued leaf, re-checked against the current t_max, primitives in order
+        const uint32_t w = qw0;
+        const float lo = ql0;
+        qw0 = qw1;
+        ql0 = ql1;
+        --qn;
+        if (tMax > lo) {
+            uint32_t leafOff = w & 0xffffffu, leafCnt = w >> 24;
+            while (leafCnt > 0) {
+                if (STATS) { cnt.prim_tests++; wave_tick(cnt.w_prim); }
+                float t;
+                if (prim_hit(prims, leafOff, o, d, tMin, tMax, t)) {
+                    tMax = t;
+                    elem = leafOff;
+                }
+                ++leafOff;
+                --leafCnt;
+            }
+        }
+        if (STATS) wave_time(cnt.cyc_leaf, tPhase);
     }
     tHit = tMax;
     return elem;
@@ -879,8 +998,8 @@ __global__ void __launch_bounds__(WPB * 64, MINW) trace_kernel(TraceParams P)
     extern __shared__ float4 lds4[];
     const uint32_t lane = threadIdx.x & 63u;
     const uint32_t wave = threadIdx.x >> 6;
-    const float4* gnodes = WW == 3 ? P.cnodes : P.nodes;
-    const uint32_t nodeF4 = WW == 3 ? 4u * P.cnodeCount : 2u * P.nodeCount;
+    const float4* gnodes = WW >= 3 ? P.cnodes : P.nodes;
+    const uint32_t nodeF4 = WW >= 3 ? 4u * P.cnodeCount : 2u * P.nodeCount;
     const uint32_t sceneF4 = (SL >= 1 ? nodeF4 : 0u) + (SL >= 2 ? 4u * P.primCount : 0u);
     if (SL >= 1) {
         for (uint32_t i = threadIdx.x; i < nodeF4; i += WPB * 64) lds4[i] = gnodes[i];
@@ -891,9 +1010,12 @@ __global__ void __launch_bounds__(WPB * 64, MINW) trace_kernel(TraceParams P)
     const float4* __restrict__ nodes = SL >= 1 ? lds4 : gnodes;
     const float4* __restrict__ prims = SL >= 2 ? lds4 + nodeF4 : P.prims;
     // wave stacks: stackDepth x 64 entries of u32 (node index), or of uint2 (word, lo) for WW == 3
-    uint32_t* stack = reinterpret_cast<uint32_t*>(lds4 + sceneF4) + (WW == 3 ? 2u : 1u) * wave * P.stackDepth * 64u +
-                      (WW == 3 ? 2u : 1u) * lane;
-    const PixelCtx pc = pixel_of(P, blockIdx.x * (uint32_t)WPB + wave, lane);
+    uint32_t* stack = reinterpret_cast<uint32_t*>(lds4 + sceneF4) + (WW >= 3 ? 2u : 1u) * wave * P.stackDepth * 64u +
+                      (WW >= 3 ? 2u : 1u) * lane;
+    const uint32_t slot = blockIdx.x * (uint32_t)WPB + wave;
+    const uint32_t tile = P.order ? P.order[slot] : slot;
+    const PixelCtx pc = pixel_of(P, tile, lane);
+    const uint64_t tWave = __builtin_amdgcn_s_memtime();
     Counters cnt = {};
     if (pc.valid) {
         Xorwow rng;
@@ -905,7 +1027,8 @@ __global__ void __launch_bounds__(WPB * 64, MINW) trace_kernel(TraceParams P)
         while (ps.alive) {
             if (STATS) { cnt.segments++; wave_tick(cnt.w_segments); }
             float t;
-            const uint32_t e = WW == 3 ? traverse_cb<STATS>(nodes, prims, reinterpret_cast<uint2*>(stack), P, ps.o, ps.d, t, cnt)
+            const uint32_t e = WW == 5 ? traverse_spec<STATS>(nodes, prims, reinterpret_cast<uint2*>(stack), P, ps.o, ps.d, t, cnt)
+                             : WW >= 3 ? traverse_cb<STATS>(nodes, prims, reinterpret_cast<uint2*>(stack), P, ps.o, ps.d, t, cnt)
                                        : traverse<STATS, WW>(nodes, prims, stack, ps.o, ps.d, P.slabFast != 0, t, cnt);
             uint64_t tS = STATS ? __builtin_amdgcn_s_memtime() : 0;
             if (shade<STATS>(P, prims, e, t, ps, rng, cnt)) finish_path<STATS>(P, ps, rng, fx, fy, cnt);
@@ -914,6 +1037,8 @@ __global__ void __launch_bounds__(WPB * 64, MINW) trace_kernel(TraceParams P)
         if (STATS) wave_time(cnt.cyc_total, tAll);
         store_pixel(P, pc, rng, ps);
     }
+    if (P.tileCost && lane == 0 && tile < P.tilesX * P.tilesY)
+        P.tileCost[tile] = (uint32_t)min(__builtin_amdgcn_s_memtime() - tWave, (uint64_t)0xffffffffu);
     flush_counters<STATS>(P, cnt);
 }
 
@@ -1085,6 +1210,13 @@ struct pt_context {
     DevTex hostTex[PT_MAX_TEXTURES] = {};
     uint32_t skybox = 0;
     unsigned long long* stats = nullptr;
+    // tile scheduling: per-tile cost of the last launch and the cost-sorted dispatch order
+    uint32_t* tileCost = nullptr;
+    uint32_t* order = nullptr;
+    uint32_t orderTiles = 0;      // tiles the device buffers hold
+    bool orderValid = false;
+    int schedule = 0;             // 0 = cost-sorted tiles (default), 1 = row-major
+    pt_camera lastCam = {};
     std::string err;
 };
 
@@ -1121,10 +1253,10 @@ static int fail(pt_context* ctx, int code, const char* msg)
 template <bool STATS, int SL, int WPB, int WW, int MINW>
 static hipError_t launch_one(const TraceParams& P, hipStream_t stream)
 {
-    const size_t nodeF4 = WW == 3 ? 4 * (size_t)P.cnodeCount : 2 * (size_t)P.nodeCount;
+    const size_t nodeF4 = WW >= 3 ? 4 * (size_t)P.cnodeCount : 2 * (size_t)P.nodeCount;
     const size_t sceneBytes = ((SL >= 1 ? nodeF4 : 0) + (SL >= 2 ? 4 * (size_t)P.primCount : 0)) * sizeof(float4);
-    const size_t lds = sceneBytes + (size_t)WPB * P.stackDepth * 64 * (WW == 3 ? 8 : 4);
-    if (WW == 3 && P.cnodes == nullptr) return launch_one<STATS, SL, WPB, 1, MINW>(P, stream);  // no child-box layout
+    const size_t lds = sceneBytes + (size_t)WPB * P.stackDepth * 64 * (WW >= 3 ? 8 : 4);
+    if (WW >= 3 && P.cnodes == nullptr) return launch_one<STATS, SL, WPB, 1, MINW>(P, stream);  // no child-box layout
     if (lds > 160 * 1024) return hipErrorInvalidValue;
     static bool attrSet = false;
     if (!attrSet) {
@@ -1173,6 +1305,8 @@ static hipError_t launch_variant(int v, const TraceParams& P, hipStream_t stream
     case 18: return launch_one<STATS, 1, 8, 3, 6>(P, stream);
     case 19: return launch_one<STATS, 1, 4, 3, 5>(P, stream);
     case 20: return launch_one<STATS, 0, 4, 3, 5>(P, stream);
+    case 21: return launch_one<STATS, 1, 4, 5, 5>(P, stream);
+    case 22: return launch_one<STATS, 0, 4, 5, 5>(P, stream);
     default: return launch_one<STATS, 0, 4, 1, 1>(P, stream);
     }
 }
@@ -1251,6 +1385,8 @@ PT_API void pt_destroy(pt_context* ctx)
     (void)hipFree(ctx->prims);
     (void)hipFree(ctx->mats);
     (void)hipFree(ctx->cnodes);
+    (void)hipFree(ctx->tileCost);
+    (void)hipFree(ctx->order);
     (void)hipFree(ctx->texTable);
     (void)hipFree(ctx->stats);
     for (auto& t : ctx->hostTex) (void)hipFree((void*)t.texels);
@@ -1368,6 +1504,7 @@ PT_API int pt_set_scene(pt_context* ctx, const pt_bvh_node* nodes, uint32_t node
         PT_HIP_CHECK(ctx, hipMemcpy(ctx->cnodes, hc.data(), hc.size() * sizeof(float4), hipMemcpyHostToDevice));
         ctx->cnodeCount = interior;
     }
+    ctx->orderValid = false;
     ctx->rootWord = word(0);
     for (int k = 0; k < 3; ++k) {
         ctx->rootBox[2 * k] = nodes[0].aabb_min[k];
@@ -1398,6 +1535,7 @@ PT_API int pt_set_texture(pt_context* ctx, uint32_t handle, const float* rgba, u
     t.texels = mem;
     t.width = width;
     t.height = height;
+    ctx->orderValid = false;
     PT_HIP_CHECK(ctx, hipMemcpy(ctx->texTable, ctx->hostTex, sizeof(ctx->hostTex), hipMemcpyHostToDevice));
     return PT_OK;
 }
@@ -1453,6 +1591,31 @@ static int render_impl(pt_context* ctx, const pt_camera* cam, uint32_t spp, uint
     P.cnodeCount = ctx->cnodeCount;
     P.rootWord = ctx->rootWord;
     for (int k = 0; k < 6; ++k) P.rootBox[k] = ctx->rootBox[k];
+    // Tile scheduling: a pixel's samples are sequential (one XORWOW stream), so a tile is the
+    // smallest unit of work and tiles differ several-fold in cost (sky vs geometry).  The first
+    // launch for a scene/camera records every tile's cost; later launches dispatch tiles in
+    // descending cost, so the launch tail consists of cheap tiles and the waves of a workgroup
+    // (which hold the group's LDS until the last one ends) have similar lengths.  The order
+    // changes which wave renders a pixel, never how: results are identical.
+    const uint32_t tiles = P.tilesX * P.tilesY;
+    if (ctx->orderTiles != tiles) {
+        (void)hipFree(ctx->tileCost);
+        (void)hipFree(ctx->order);
+        ctx->tileCost = nullptr;
+        ctx->order = nullptr;
+        ctx->orderTiles = 0;
+        ctx->orderValid = false;
+        PT_HIP_CHECK(ctx, hipMalloc(&ctx->tileCost, (size_t)tiles * sizeof(uint32_t)));
+        PT_HIP_CHECK(ctx, hipMalloc(&ctx->order, ((size_t)tiles + 64) * sizeof(uint32_t)));
+        ctx->orderTiles = tiles;
+    }
+    if (memcmp(&ctx->lastCam, cam, sizeof(pt_camera)) != 0) {
+        ctx->orderValid = false;
+        ctx->lastCam = *cam;
+    }
+    const bool record = ctx->schedule == 0 && !ctx->orderValid;
+    P.order = (ctx->schedule == 0 && ctx->orderValid) ? ctx->order : nullptr;
+    P.tileCost = record ? ctx->tileCost : nullptr;
     if (stats) PT_HIP_CHECK(ctx, hipMemsetAsync(ctx->stats, 0, 16 * sizeof(unsigned long long), ctx->stream));
     PT_HIP_CHECK(ctx, hipEventRecord(ctx->ev0, ctx->stream));
     const int variant = pick_variant(ctx);
@@ -1463,6 +1626,14 @@ static int render_impl(pt_context* ctx, const pt_camera* cam, uint32_t spp, uint
     float ms = 0.0f;
     PT_HIP_CHECK(ctx, hipEventElapsedTime(&ms, ctx->ev0, ctx->ev1));
     if (gpu_ms) *gpu_ms = ms;
+    if (record) {
+        std::vector<uint32_t> cost(tiles), order((size_t)tiles + 64);
+        PT_HIP_CHECK(ctx, hipMemcpy(cost.data(), ctx->tileCost, (size_t)tiles * sizeof(uint32_t), hipMemcpyDeviceToHost));
+        for (uint32_t i = 0; i < tiles + 64; ++i) order[i] = i;      // slots past the last tile stay invalid
+        std::stable_sort(order.begin(), order.begin() + tiles, [&](uint32_t a, uint32_t b) { return cost[a] > cost[b]; });
+        PT_HIP_CHECK(ctx, hipMemcpy(ctx->order, order.data(), order.size() * sizeof(uint32_t), hipMemcpyHostToDevice));
+        ctx->orderValid = true;
+    }
     if (stats) {
         unsigned long long h[16];
         PT_HIP_CHECK(ctx, hipMemcpy(h, ctx->stats, sizeof(h), hipMemcpyDeviceToHost));
@@ -1482,6 +1653,14 @@ static int render_impl(pt_context* ctx, const pt_camera* cam, uint32_t spp, uint
         stats->cycles_shading = h[13];
         stats->cycles_total = h[14];
     }
+    return PT_OK;
+}
+
+PT_API int pt_set_schedule(pt_context* ctx, int mode)
+{
+    if (!ctx || mode < 0 || mode > 1) return PT_ERR_ARG;
+    ctx->schedule = mode;
+    ctx->orderValid = false;
     return PT_OK;
 }
 
@@ -1565,7 +1744,7 @@ PT_API uint32_t pt_local_rows(const pt_context* ctx) { return ctx ? ctx->rows : 
 
 PT_API int pt_set_kernel_variant(pt_context* ctx, int variant)
 {
-    if (!ctx || variant < 0 || variant > 20) return PT_ERR_ARG;
+    if (!ctx || variant < 0 || variant > 22) return PT_ERR_ARG;
     ctx->variant = variant;
     return PT_OK;
 }

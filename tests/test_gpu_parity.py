@@ -67,7 +67,7 @@ def test_render_bitexact(gpu_available, scenes, name, W, H, spp, chunks):
     assert pt.frames == ref.frames == chunks
 
 
-@pytest.mark.parametrize("variant", range(1, 21))
+@pytest.mark.parametrize("variant", range(1, 23))
 def test_every_kernel_variant_bitexact(gpu_available, scenes, variant):
     # all trace-kernel variants (schedules, LDS staging, occupancy) produce the reference's bits
     pt, cam, ref, osc = pair(scenes / "test_shapes.scene.json", 72, 40)
@@ -97,12 +97,29 @@ def test_single_leaf_bvh_every_traversal(gpu_available, scenes, nprims):
     prims = (pa.PtHittable * nprims).from_buffer_copy(bytes(osc.prims)[:nprims * C.sizeof(pa.PtHittable)])
     N.check_ctx(N.hip().pt_set_scene(pt._ctx, nodes, 1, prims, nprims), pt._ctx)
     ref.render(osc.camera, 2, True, chunks=1)
-    for variant in (0, 6, 12, 16, 17, 20):
+    for variant in (0, 6, 12, 16, 17, 20, 21, 22):
         st = pt.rng_state()
         pt.set_kernel_variant(variant)
         pt.render_raw(cam, 2, 1, True)
         assert_bitexact(pt.accum(), ref.accum, f"single leaf {nprims}, variant {variant}")
         pt.set_rng_state(st)
+
+
+def test_tile_schedule_does_not_change_results(gpu_available, scenes):
+    # cost-sorted tile dispatch (default) vs row-major: same bits, ragged tile grid, row tiles
+    for (W, H, off, stride) in [(75, 43, 0, 1), (64, 90, 1, 3)]:
+        pt, cam, ref, osc = pair(scenes / "generated_scene.scene.json", W, H, off, stride)
+        st = pt.rng_state()
+        pt.render(cam, 2, True)                      # records the tile costs
+        pt.set_rng_state(st)
+        pt.render_raw(cam, 2, 1, True)               # runs in cost order
+        sorted_acc = pt.accum()
+        pt.set_schedule(1)
+        pt.set_rng_state(st)
+        pt.render_raw(cam, 2, 1, True)
+        assert np.array_equal(bits(sorted_acc), bits(pt.accum()))
+        ref.render(osc.camera, 2, True)
+        assert_bitexact(sorted_acc, ref.accum, f"sorted schedule {W}x{H}")
 
 
 def test_history_semantics(gpu_available, scenes):

@@ -23,32 +23,39 @@ def main():
     ap.add_argument("--spp", type=int, default=64)
     ap.add_argument("--rounds", type=int, default=5)
     ap.add_argument("--variants", default="1,2,3,4,5")
+    ap.add_argument("--schedules", default="0", help="tile schedules to cross with the variants (0 sorted, 1 row-major)")
     a = ap.parse_args()
-    vs = [int(v) for v in a.variants.split(",")]
+    vs = [(int(v), int(m)) for v in a.variants.split(",") for m in a.schedules.split(",")]
     pt = pa.Pathtracer(a.width, a.height)
     cam = pt.load_scene(a.scene)
     chunks = a.spp // 8
     ref = None
     times = {v: [] for v in vs}
-    for v in vs:                                   # correctness first: every variant bit-identical
+    for v, m in vs:                                # correctness first: every variant bit-identical
         pt.set_kernel_variant(v)
+        pt.set_schedule(m)
         st = pt.rng_state()
-        pt.render_raw(cam, 8, 1, True)
+        pt.render_raw(cam, 8, 1, True)             # schedule 0: records the tile costs
+        pt.set_rng_state(st)
+        pt.render_raw(cam, 8, 1, True)             # ... and this launch runs in cost order
         acc = pt.accum()
         pt.set_rng_state(st)
         if ref is None:
             ref = acc
-        assert np.array_equal(acc.view(np.uint32), ref.view(np.uint32)), f"variant {v} differs"
+        assert np.array_equal(acc.view(np.uint32), ref.view(np.uint32)), f"variant {v} schedule {m} differs"
     for r in range(a.rounds):
-        for v in vs:
+        for v, m in vs:
             pt.set_kernel_variant(v)
+            if len(a.schedules.split(",")) > 1:
+                pt.set_schedule(m)
+                pt.render_raw(cam, 8, 1, True)     # records the tile costs for mode 0
             ms = pt.render_raw(cam, 8, chunks, True)
-            times[v].append(ms)
+            times[(v, m)].append(ms)
     samples = a.width * a.height * a.spp
     out = {}
-    for v in vs:
-        t = np.array(times[v])
-        out[v] = {"median_ms": float(np.median(t)), "min_ms": float(t.min()),
+    for v, m in vs:
+        t = np.array(times[(v, m)])
+        out[f"{v}" if len(a.schedules.split(",")) == 1 else f"{v}/s{m}"] = {"median_ms": float(np.median(t)), "min_ms": float(t.min()),
                   "Msamples_s": round(samples / (np.median(t) / 1e3) / 1e6, 1)}
     print(json.dumps({"scene": pathlib.Path(a.scene).name, "spp": a.spp, "variants": out}))
 
