@@ -54,15 +54,21 @@ def algorithmic_bytes(stats: dict, pixels: int, launches: int) -> float:
 
 
 def load_pmc_traffic(workload: str):
-    """Per-launch HBM bytes of the trace kernel from the committed rocprofv3 --pmc summary."""
+    """Per-launch HBM bytes of the trace kernel from the committed rocprofv3 --pmc summary, and the
+    VALU issue fraction of the same launch: wave64 VALU instructions x 4 cycles (SIMD16) over
+    1024 SIMDs x shader-active cycles (GRBM_GUI_ACTIVE summed over the 8 XCDs)."""
     for f in sorted((ROOT / "profiles").glob("*pmc_traffic*.json"), reverse=True):
         try:
             d = json.loads(f.read_text())
         except (OSError, ValueError):
             continue
         if d.get("workload") == workload and d.get("bytes_per_launch"):
-            return float(d["bytes_per_launch"]), f.name
-    return None, None
+            c = d.get("counters", {})
+            valu = None
+            if c.get("SQ_INSTS_VALU") and c.get("GRBM_GUI_ACTIVE"):
+                valu = round(4.0 * c["SQ_INSTS_VALU"] / (1024.0 * c["GRBM_GUI_ACTIVE"] / 8.0), 3)
+            return float(d["bytes_per_launch"]), f.name, valu
+    return None, None, None
 
 
 def cpu_baseline(args, W, H):
@@ -128,8 +134,12 @@ def main():
         if dist_on:
             dist.barrier()
 
-    # instrumented run (not timed): algorithmic byte count of this workload, 1 chunk
+    # instrumented run (not timed): algorithmic byte count of this workload, 1 chunk.  Counted
+    # with the non-speculative child-box kernel, whose node/primitive tests are the reference's
+    # (the speculative variant adds node tests of its own); then back to automatic selection.
+    pt.set_kernel_variant(20)
     stats = pt.render_instrumented(cam, chunk, 1, True)
+    pt.set_kernel_variant(0)    # (that launch also recorded the tile costs: every timed launch is cost-ordered)
     samples_per_chunk = stats["samples"]
     for _ in range(args.warmup):
         step()
@@ -159,7 +169,7 @@ def main():
     avg_launch_s = kernel_ms / args.steps / 1e3
     achieved = per_gpu_bytes / avg_launch_s / 1e9
     workload = f"generated_scene {W}x{H} {spp}spp chunk{chunk}"
-    traffic, traffic_src = load_pmc_traffic(workload)
+    traffic, traffic_src, valu_frac = load_pmc_traffic(workload)
     out = {
         "metric": "Msamples/sec + achieved HBM GB/s, 1080p 1024spp, 1/2/4/8 MI355X",
         "value": round(value, 3),
@@ -179,7 +189,11 @@ def main():
                      "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic,
                      "kernel": "trace_kernel", "avg_launch_ms": round(avg_launch_s * 1e3, 3),
                      "bytes_per_sample": round(launch_bytes / (W * H * spp), 1),
-                     "traffic_source": traffic_src},
+                     "traffic_source": traffic_src,
+                     # the algorithmic bytes are served from LDS and L2 (traffic = HBM bytes measured);
+                     # the kernel is bound by VALU issue, whose busy fraction the same profile gives
+                     "hbm_frac_measured": (round(traffic / avg_launch_s / 1e9 / HBM_PEAK_GBS, 5) if traffic else None),
+                     "valu_issue_frac": valu_frac},
         "cpu_baseline": None,
     }
     if rank == 0 and n == 1 and args.cpu_baseline:

@@ -1319,8 +1319,9 @@ static int pick_variant(const pt_context* ctx)
     // wins on every scene; the child-box records are staged in LDS when they fit in 48 KB
     // (cornell, the 484-object scene) and read through the caches otherwise (100k objects).
     // Scenes outside the child-box encoding fall back to the node-at-a-time walk (launch_one).
+    // Deep BVHs read through the caches gain from speculative traversal (variant 22).
     const size_t cbBytes = 4 * (size_t)ctx->cnodeCount * sizeof(float4);
-    if (ctx->cnodes) return cbBytes <= 48 * 1024 ? 19 : 20;
+    if (ctx->cnodes) return cbBytes <= 48 * 1024 ? 19 : 22;
     const size_t nodeBytes = 2 * (size_t)ctx->nodeCount * sizeof(float4);
     return nodeBytes <= 48 * 1024 ? 6 : 4;
 }
