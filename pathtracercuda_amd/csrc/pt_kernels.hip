@@ -530,6 +530,109 @@ PT_DEV uint32_t traverse_cb(const float4* __restrict__ cnodes, const float4* __r
 }
 
 // ---------------------------------------------------------------------------------------------
+// Resumable child-box traversal (WW = 100 + Q).  The wave leaves the traversal as soon as at most
+// Q/64 of the lanes that entered are still walking, shades the finished ones, and resumes the stragglers'
+// traversals -- node, stack pointer, t_max, closest primitive; the stack itself stays in LDS --
+// together with the new rays of the shaded lanes.  The long tail of a wave's traversal (a few
+// lanes with deep walks while the rest idle) then overlaps other lanes' next segments.  Every
+// lane performs exactly the same sequence of tests as traverse_cb; only when differs.
+// ---------------------------------------------------------------------------------------------
+struct TravState {
+    uint32_t cur, sp, elem;
+    float tMax;
+};
+
+template <bool STATS, int EXITQ>
+PT_DEV bool traverse_cb_phase(const float4* __restrict__ cnodes, const float4* __restrict__ prims, uint2* stack,
+                              const TraceParams& P, f3 o, f3 d, bool fresh, TravState& ts, Counters& cnt)
+{
+    const float tMin = 0.001f;
+    SlabRay R;
+    R.o = o;
+    R.ix = 1.0f / d.x;
+    R.iy = 1.0f / d.y;
+    R.iz = 1.0f / d.z;
+    R.fast = P.slabFast && __builtin_isfinite(R.ix) && __builtin_isfinite(R.iy) && __builtin_isfinite(R.iz);
+    R.ox2 = f2(o.x, o.x);
+    R.oy2 = f2(o.y, o.y);
+    R.oz2 = f2(o.z, o.z);
+    R.ix2 = f2(R.ix, R.ix);
+    R.iy2 = f2(R.iy, R.iy);
+    R.iz2 = f2(R.iz, R.iz);
+    const uint32_t negMask = (d.x < 0.0f ? 1u : 0u) | (d.y < 0.0f ? 2u : 0u) | (d.z < 0.0f ? 4u : 0u);
+    const uint32_t nAct = (uint32_t)__popcll(__ballot(1));
+    bool done = false;
+    if (fresh) {
+        ts.tMax = kFltMax;
+        ts.sp = 0;
+        ts.elem = 0xffffffffu;
+        ts.cur = P.rootWord;
+        if (STATS) { cnt.node_tests++; wave_tick(cnt.w_node); }
+        float X;
+        const float lo0 = slab_lo_x(R, f2(P.rootBox[0], P.rootBox[1]), f2(P.rootBox[2], P.rootBox[3]),
+                                    f2(P.rootBox[4], P.rootBox[5]), tMin, X);
+        done = !(X > lo0 && ts.tMax > lo0);
+    }
+    uint32_t sp = ts.sp, cur = ts.cur, elem = ts.elem;
+    float tMax = ts.tMax;
+    auto pop = [&]() -> bool {
+        while (sp > 0) {
+            const uint2 e = stack[64u * (--sp)];
+            if (tMax > __uint_as_float(e.y)) { cur = e.x; return true; }
+        }
+        return false;
+    };
+    while (!done) {
+        while ((cur >> 24) == 0u) {                               // interior walk
+            if (STATS) { cnt.node_tests += 2; wave_tick(cnt.w_node); }
+            const float4 Q0 = cnodes[4 * cur], Q1 = cnodes[4 * cur + 1];
+            const float4 Q2 = cnodes[4 * cur + 2], Q3 = cnodes[4 * cur + 3];
+            float XL, XR;
+            const float loL = slab_lo_x(R, f2(Q0.x, Q0.y), f2(Q0.z, Q0.w), f2(Q1.x, Q1.y), tMin, XL);
+            const float loR = slab_lo_x(R, f2(Q2.x, Q2.y), f2(Q2.z, Q2.w), f2(Q1.z, Q1.w), tMin, XR);
+            const bool hL = XL > loL && tMax > loL, hR = XR > loR && tMax > loR;
+            const bool isNeg = (negMask >> __float_as_uint(Q3.z)) & 1u;
+            const uint32_t wL = __float_as_uint(Q3.x), wR = __float_as_uint(Q3.y);
+            const bool hN = isNeg ? hR : hL, hF = isNeg ? hL : hR;
+            const uint32_t wN = isNeg ? wR : wL, wF = isNeg ? wL : wR;
+            const float loF = isNeg ? loL : loR;
+            if (hN) {
+                if (hF) {
+                    stack[64u * sp] = make_uint2(wF, __float_as_uint(loF));
+                    ++sp;
+                }
+                cur = wN;
+            } else if (hF) {
+                cur = wF;
+            } else if (!pop()) {
+                done = true;
+                break;
+            }
+        }
+        if (done) break;
+        uint32_t leafOff = cur & 0xffffffu, leafCnt = cur >> 24;
+        while (leafCnt > 0) {
+            if (STATS) { cnt.prim_tests++; wave_tick(cnt.w_prim); }
+            float t;
+            if (prim_hit(prims, leafOff, o, d, tMin, tMax, t)) {
+                tMax = t;
+                elem = leafOff;
+            }
+            ++leafOff;
+            --leafCnt;
+        }
+        if (!pop()) { done = true; break; }
+        // early exit once at most EXITQ/64 of the lanes that entered are still walking
+        if ((uint32_t)__popcll(__ballot(1)) * 64u <= nAct * (uint32_t)EXITQ) break;
+    }
+    ts.sp = sp;
+    ts.cur = cur;
+    ts.elem = elem;
+    ts.tMax = tMax;
+    return done;
+}
+
+// ---------------------------------------------------------------------------------------------
 // Speculative child-box traversal (WW == 5).  While some lane of the wave still searches for its
 // next leaf, lanes that already hold one keep walking and queue a second leaf (Aila & Laine's
 // speculative traversal).  Exactness: child boxes are nested (a parent's bounds are the union of
@@ -1024,7 +1127,21 @@ __global__ void __launch_bounds__(WPB * 64, MINW) trace_kernel(TraceParams P)
         const float fx = (float)(int32_t)pc.px, fy = (float)(int32_t)pc.py;
         camera_ray(P, fx, fy, rng, ps.o, ps.d);
         uint64_t tAll = STATS ? __builtin_amdgcn_s_memtime() : 0;
-        while (ps.alive) {
+        if (WW >= 100) {
+            bool fresh = true;
+            TravState ts = {0u, 0u, 0xffffffffu, kFltMax};
+            while (ps.alive) {
+                if (STATS && fresh) { cnt.segments++; wave_tick(cnt.w_segments); }
+                const bool tdone = traverse_cb_phase<STATS, WW - 100>(nodes, prims, reinterpret_cast<uint2*>(stack), P,
+                                                                        ps.o, ps.d, fresh, ts, cnt);
+                fresh = tdone;
+                if (!tdone) continue;                              // suspended: resumes next round
+                uint64_t tS = STATS ? __builtin_amdgcn_s_memtime() : 0;
+                if (shade<STATS>(P, prims, ts.elem, ts.tMax, ps, rng, cnt)) finish_path<STATS>(P, ps, rng, fx, fy, cnt);
+                if (STATS) wave_time(cnt.cyc_shade, tS);
+            }
+        }
+        while (WW < 100 && ps.alive) {
             if (STATS) { cnt.segments++; wave_tick(cnt.w_segments); }
             float t;
             const uint32_t e = WW == 5 ? traverse_spec<STATS>(nodes, prims, reinterpret_cast<uint2*>(stack), P, ps.o, ps.d, t, cnt)
@@ -1307,6 +1424,13 @@ static hipError_t launch_variant(int v, const TraceParams& P, hipStream_t stream
     case 20: return launch_one<STATS, 0, 4, 3, 5>(P, stream);
     case 21: return launch_one<STATS, 1, 4, 5, 5>(P, stream);
     case 22: return launch_one<STATS, 0, 4, 5, 5>(P, stream);
+    case 23: return launch_one<STATS, 1, 4, 116, 5>(P, stream);  // resumable: exit at <= 16/64 walking
+    case 24: return launch_one<STATS, 1, 4, 104, 5>(P, stream);  // <= 4/64
+    case 25: return launch_one<STATS, 1, 4, 108, 5>(P, stream);  // <= 8/64
+    case 26: return launch_one<STATS, 0, 4, 108, 5>(P, stream);
+    case 27: return launch_one<STATS, 1, 4, 102, 5>(P, stream);  // <= 2/64
+    case 28: return launch_one<STATS, 1, 4, 112, 5>(P, stream);  // <= 12/64
+    case 29: return launch_one<STATS, 1, 4, 108, 6>(P, stream);
     default: return launch_one<STATS, 0, 4, 1, 1>(P, stream);
     }
 }
@@ -1319,9 +1443,11 @@ static int pick_variant(const pt_context* ctx)
     // wins on every scene; the child-box records are staged in LDS when they fit in 48 KB
     // (cornell, the 484-object scene) and read through the caches otherwise (100k objects).
     // Scenes outside the child-box encoding fall back to the node-at-a-time walk (launch_one).
-    // Deep BVHs read through the caches gain from speculative traversal (variant 22).
+    // With the records in LDS the resumable form (variant 28: the wave shades its finished lanes
+    // once at most 12/64 still walk) wins; deep BVHs read through the caches gain most from
+    // speculative traversal (variant 22).
     const size_t cbBytes = 4 * (size_t)ctx->cnodeCount * sizeof(float4);
-    if (ctx->cnodes) return cbBytes <= 48 * 1024 ? 19 : 22;
+    if (ctx->cnodes) return cbBytes <= 48 * 1024 ? 28 : 22;
     const size_t nodeBytes = 2 * (size_t)ctx->nodeCount * sizeof(float4);
     return nodeBytes <= 48 * 1024 ? 6 : 4;
 }
@@ -1745,7 +1871,7 @@ PT_API uint32_t pt_local_rows(const pt_context* ctx) { return ctx ? ctx->rows : 
 
 PT_API int pt_set_kernel_variant(pt_context* ctx, int variant)
 {
-    if (!ctx || variant < 0 || variant > 22) return PT_ERR_ARG;
+    if (!ctx || variant < 0 || variant > 29) return PT_ERR_ARG;
     ctx->variant = variant;
     return PT_OK;
 }

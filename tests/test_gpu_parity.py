@@ -67,7 +67,7 @@ def test_render_bitexact(gpu_available, scenes, name, W, H, spp, chunks):
     assert pt.frames == ref.frames == chunks
 
 
-@pytest.mark.parametrize("variant", range(1, 23))
+@pytest.mark.parametrize("variant", range(1, 30))
 def test_every_kernel_variant_bitexact(gpu_available, scenes, variant):
     # all trace-kernel variants (schedules, LDS staging, occupancy) produce the reference's bits
     pt, cam, ref, osc = pair(scenes / "test_shapes.scene.json", 72, 40)
@@ -97,7 +97,7 @@ def test_single_leaf_bvh_every_traversal(gpu_available, scenes, nprims):
     prims = (pa.PtHittable * nprims).from_buffer_copy(bytes(osc.prims)[:nprims * C.sizeof(pa.PtHittable)])
     N.check_ctx(N.hip().pt_set_scene(pt._ctx, nodes, 1, prims, nprims), pt._ctx)
     ref.render(osc.camera, 2, True, chunks=1)
-    for variant in (0, 6, 12, 16, 17, 20, 21, 22):
+    for variant in (0, 6, 12, 16, 17, 20, 21, 22, 25, 26):
         st = pt.rng_state()
         pt.set_kernel_variant(variant)
         pt.render_raw(cam, 2, 1, True)
