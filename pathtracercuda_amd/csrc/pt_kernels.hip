@@ -582,6 +582,7 @@ PT_DEV bool traverse_cb_phase(const float4* __restrict__ cnodes, const float4* _
         }
         return false;
     };
+    uint64_t tPhase = STATS ? __builtin_amdgcn_s_memtime() : 0;
     while (!done) {
         while ((cur >> 24) == 0u) {                               // interior walk
             if (STATS) { cnt.node_tests += 2; wave_tick(cnt.w_node); }
@@ -609,6 +610,7 @@ PT_DEV bool traverse_cb_phase(const float4* __restrict__ cnodes, const float4* _
                 break;
             }
         }
+        if (STATS) wave_time(cnt.cyc_node, tPhase);
         if (done) break;
         uint32_t leafOff = cur & 0xffffffu, leafCnt = cur >> 24;
         while (leafCnt > 0) {
@@ -621,6 +623,7 @@ PT_DEV bool traverse_cb_phase(const float4* __restrict__ cnodes, const float4* _
             ++leafOff;
             --leafCnt;
         }
+        if (STATS) wave_time(cnt.cyc_leaf, tPhase);
         if (!pop()) { done = true; break; }
         // early exit once at most EXITQ/64 of the lanes that entered are still walking
         if ((uint32_t)__popcll(__ballot(1)) * 64u <= nAct * (uint32_t)EXITQ) break;
@@ -821,32 +824,20 @@ PT_DEV void tangent_frame(f3 N, f3& t, f3& b)
     b = cross(N, t);
 }
 
-PT_DEV f3 cosine_sample(float u0, float u1)   // MonteCarlo.h:24-30
-{
-    const float phi = kTwoPi * u0;
-    const float cosTheta = sqrtf(u1);
-    const float sinTheta = sqrtf(1.0f - u1);
-    float s, c;
-    sincos_pos(phi, s, c);
-    return mk(c * sinTheta, s * sinTheta, cosTheta);
-}
-
 PT_DEV float d_ggx(float NdotH, float a2)     // brdf.h:11-15
 {
     const float dd = (NdotH * a2 - NdotH) * NdotH + 1.0f;
     return a2 / (kPi * dd * dd);
 }
 
-PT_DEV f3 vndf_sample(f3 V, float u0, float u1, float a)   // MonteCarlo.h:73-101
+// importanceSampleGGXVNDF (MonteCarlo.h:73-101) with r = sqrt(u0) and (sin, cos)(2 pi u1) supplied
+// by the caller (shared with the cosine lobe, MonteCarlo.h:24-30, see shade)
+PT_DEV f3 vndf_sample_rsc(f3 V, float r, float s, float c, float a)
 {
     const f3 Vh = normalize(mk(a * V.x, a * V.y, V.z));
     const float lensq = Vh.x * Vh.x + Vh.y * Vh.y;
     const f3 T1 = lensq > 0.0f ? scale(1.0f / sqrtf(lensq), mk(-Vh.y, Vh.x, 0.0f)) : mk(1.0f, 0.0f, 0.0f);
     const f3 T2 = cross(Vh, T1);
-    const float r = sqrtf(u0);
-    const float phi = kTwoPi * u1;
-    float s, c;
-    sincos_pos(phi, s, c);
     const float t1 = r * c;
     float t2 = r * s;
     const float sv = 0.5f * (1.0f + Vh.z);
@@ -955,18 +946,28 @@ PT_DEV bool shade(const TraceParams& P, const float4* __restrict__ prims, uint32
     f3 dir = splat(0.0f), att = splat(0.0f);
     float pdf = 0.0f;
     bool killed = false;
+    // Lobe sampling.  cosine_sample(u0, u1) needs sincos(2 pi u0) and sqrt(u1); vndf_sample(u0, u1)
+    // needs sqrt(u0) and sincos(2 pi u1): one shared sincos and sqrt with per-lane operands serve
+    // both lobes (a wave shading LAMBERT_GGX runs both), each lane computing exactly its own lobe.
+    bool specular = mtype == 1u;
+    if (mtype == 2u) {                                                        // LAMBERT_GGX (:101-144)
+        if (rnd0 < 0.5f) rnd0 = 2.0f * rnd0;
+        else { rnd0 = 2.0f * (rnd0 - 0.5f); specular = true; }
+    }
+    float sn, cs;
+    sincos_pos(kTwoPi * (specular ? rnd1 : rnd0), sn, cs);
+    const float sq = sqrtf(specular ? rnd0 : rnd1);
     if (mtype == 0u) {                                                        // LAMBERT (Material.inl:67-72)
-        dir = cosine_sample(rnd0, rnd1);
+        dir = mk(cs * sqrtf(1.0f - rnd1), sn * sqrtf(1.0f - rnd1), sq);       // cosine_sample
         pdf = dir.z / kPi;
         att = scale(kInvPi, base);
     } else if (mtype <= 2u) {
-        bool specular = true;
-        if (mtype == 2u) {                                                    // LAMBERT_GGX (:101-144)
-            if (rnd0 < 0.5f) { rnd0 = 2.0f * rnd0; specular = false; }
-            else rnd0 = 2.0f * (rnd0 - 0.5f);
+        if (specular) {
+            dir = reflect(neg(V), vndf_sample_rsc(V, sq, sn, cs, a));
+        } else {
+            const float sinTheta = sqrtf(1.0f - rnd1);
+            dir = mk(cs * sinTheta, sn * sinTheta, sq);
         }
-        if (specular) dir = reflect(neg(V), vndf_sample(V, rnd0, rnd1, a));
-        else dir = cosine_sample(rnd0, rnd1);
         if (dir.z < 0.0f) {
             killed = true;                                                    // pdf = 1, attenuation 0
         } else {
