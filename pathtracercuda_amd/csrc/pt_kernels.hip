@@ -401,7 +401,7 @@ PT_DEV uint32_t traverse(const float4* __restrict__ nodes, const float4* __restr
 // Child-box traversal (WW == 3).  Device layout "cnodes": one 64-byte record per INTERIOR node of
 // the reference BVH holding both children's boxes and references:
 //   Q0 = (L.min.x, L.max.x, L.min.y, L.max.y)   Q1 = (L.min.z, L.max.z, R.min.z, R.max.z)
-//   Q2 = (R.min.x, R.max.x, R.min.y, R.max.y)   Q3 = (L word, R word, split axis, 0)
+//   Q2 = (R.min.x, R.max.x, R.min.y, R.max.y)   Q3 = (L word, R word, 1 << split axis, 0)
 // L = first child (node + 1), R = second child (node.offset); a child word is (count << 24 | prim
 // offset) for a leaf and the child's record index for an interior node.
 //
@@ -448,6 +448,37 @@ PT_DEV float slab_lo_x(const SlabRay& R, f2v bx, f2v by, f2v bz, float tMin, flo
     return lo;
 }
 
+// Both children of interior record `cur`, in the reference's visit order (trace.cu:66-77: near =
+// second child when the ray direction is negative along the split axis).  The slab values are
+// put in near/far order first so that each hit flag comes straight from compares (a wave mask)
+// rather than from selects between flags, which the compiler materialises per lane.
+struct ChildPair {
+    bool hN, hF;
+    uint32_t wN, wF;
+    float loN, loF;
+};
+
+PT_DEV ChildPair cb_children(const float4* __restrict__ cnodes, uint32_t cur, const SlabRay& R, uint32_t negMask,
+                             float tMin, float tMax)
+{
+    const float4 Q0 = cnodes[4 * cur], Q1 = cnodes[4 * cur + 1];
+    const float4 Q2 = cnodes[4 * cur + 2], Q3 = cnodes[4 * cur + 3];
+    float XL, XR;
+    const float loL = slab_lo_x(R, f2(Q0.x, Q0.y), f2(Q0.z, Q0.w), f2(Q1.x, Q1.y), tMin, XL);
+    const float loR = slab_lo_x(R, f2(Q2.x, Q2.y), f2(Q2.z, Q2.w), f2(Q1.z, Q1.w), tMin, XR);
+    const bool isNeg = (negMask & __float_as_uint(Q3.z)) != 0u;
+    const uint32_t wL = __float_as_uint(Q3.x), wR = __float_as_uint(Q3.y);
+    ChildPair c;
+    c.loN = isNeg ? loR : loL;
+    c.loF = isNeg ? loL : loR;
+    const float XN = isNeg ? XR : XL, XF = isNeg ? XL : XR;
+    c.hN = XN > c.loN && tMax > c.loN;
+    c.hF = XF > c.loF && tMax > c.loF;
+    c.wN = isNeg ? wR : wL;
+    c.wF = isNeg ? wL : wR;
+    return c;
+}
+
 template <bool STATS>
 PT_DEV uint32_t traverse_cb(const float4* __restrict__ cnodes, const float4* __restrict__ prims, uint2* stack,
                             const TraceParams& P, f3 o, f3 d, float& tHit, Counters& cnt)
@@ -485,25 +516,13 @@ PT_DEV uint32_t traverse_cb(const float4* __restrict__ cnodes, const float4* __r
     while (!done) {
         while ((cur >> 24) == 0u) {                               // interior walk
             if (STATS) { cnt.node_tests += 2; wave_tick(cnt.w_node); }
-            const float4 Q0 = cnodes[4 * cur], Q1 = cnodes[4 * cur + 1];
-            const float4 Q2 = cnodes[4 * cur + 2], Q3 = cnodes[4 * cur + 3];
-            float XL, XR;
-            const float loL = slab_lo_x(R, f2(Q0.x, Q0.y), f2(Q0.z, Q0.w), f2(Q1.x, Q1.y), tMin, XL);
-            const float loR = slab_lo_x(R, f2(Q2.x, Q2.y), f2(Q2.z, Q2.w), f2(Q1.z, Q1.w), tMin, XR);
-            const bool hL = XL > loL && tMax > loL, hR = XR > loR && tMax > loR;
-            const bool isNeg = (negMask >> __float_as_uint(Q3.z)) & 1u;    // trace.cu:66-77
-            const uint32_t wL = __float_as_uint(Q3.x), wR = __float_as_uint(Q3.y);
-            const bool hN = isNeg ? hR : hL, hF = isNeg ? hL : hR;
-            const uint32_t wN = isNeg ? wR : wL, wF = isNeg ? wL : wR;
-            const float loF = isNeg ? loL : loR;
-            if (hN) {
-                if (hF) {
-                    stack[64u * sp] = make_uint2(wF, __float_as_uint(loF));
-                    ++sp;
-                }
-                cur = wN;
-            } else if (hF) {
-                cur = wF;
+            const ChildPair ch = cb_children(cnodes, cur, R, negMask, tMin, tMax);   // trace.cu:66-77
+            if (ch.hN && ch.hF) {
+                stack[64u * sp] = make_uint2(ch.wF, __float_as_uint(ch.loF));
+                ++sp;
+            }
+            if (ch.hN || ch.hF) {
+                cur = ch.hN ? ch.wN : ch.wF;
             } else if (!pop()) {
                 done = true;
                 break;
@@ -586,25 +605,13 @@ PT_DEV bool traverse_cb_phase(const float4* __restrict__ cnodes, const float4* _
     while (!done) {
         while ((cur >> 24) == 0u) {                               // interior walk
             if (STATS) { cnt.node_tests += 2; wave_tick(cnt.w_node); }
-            const float4 Q0 = cnodes[4 * cur], Q1 = cnodes[4 * cur + 1];
-            const float4 Q2 = cnodes[4 * cur + 2], Q3 = cnodes[4 * cur + 3];
-            float XL, XR;
-            const float loL = slab_lo_x(R, f2(Q0.x, Q0.y), f2(Q0.z, Q0.w), f2(Q1.x, Q1.y), tMin, XL);
-            const float loR = slab_lo_x(R, f2(Q2.x, Q2.y), f2(Q2.z, Q2.w), f2(Q1.z, Q1.w), tMin, XR);
-            const bool hL = XL > loL && tMax > loL, hR = XR > loR && tMax > loR;
-            const bool isNeg = (negMask >> __float_as_uint(Q3.z)) & 1u;
-            const uint32_t wL = __float_as_uint(Q3.x), wR = __float_as_uint(Q3.y);
-            const bool hN = isNeg ? hR : hL, hF = isNeg ? hL : hR;
-            const uint32_t wN = isNeg ? wR : wL, wF = isNeg ? wL : wR;
-            const float loF = isNeg ? loL : loR;
-            if (hN) {
-                if (hF) {
-                    stack[64u * sp] = make_uint2(wF, __float_as_uint(loF));
-                    ++sp;
-                }
-                cur = wN;
-            } else if (hF) {
-                cur = wF;
+            const ChildPair ch = cb_children(cnodes, cur, R, negMask, tMin, tMax);   // trace.cu:66-77
+            if (ch.hN && ch.hF) {
+                stack[64u * sp] = make_uint2(ch.wF, __float_as_uint(ch.loF));
+                ++sp;
+            }
+            if (ch.hN || ch.hF) {
+                cur = ch.hN ? ch.wN : ch.wF;
             } else if (!pop()) {
                 done = true;
                 break;
@@ -694,24 +701,14 @@ PT_DEV uint32_t traverse_spec(const float4* __restrict__ cnodes, const float4* _
                     }
                 } else {
                     if (STATS) { cnt.node_tests += 2; wave_tick(cnt.w_node); }
-                    const float4 Q0 = cnodes[4 * cur], Q1 = cnodes[4 * cur + 1];
-                    const float4 Q2 = cnodes[4 * cur + 2], Q3 = cnodes[4 * cur + 3];
-                    float XL, XR;
-                    const float loL = slab_lo_x(R, f2(Q0.x, Q0.y), f2(Q0.z, Q0.w), f2(Q1.x, Q1.y), tMin, XL);
-                    const float loR = slab_lo_x(R, f2(Q2.x, Q2.y), f2(Q2.z, Q2.w), f2(Q1.z, Q1.w), tMin, XR);
-                    const bool hL = XL > loL && tMax > loL, hR = XR > loR && tMax > loR;
-                    const bool isNeg = (negMask >> __float_as_uint(Q3.z)) & 1u;
-                    const uint32_t wL = __float_as_uint(Q3.x), wR = __float_as_uint(Q3.y);
-                    const bool hN = isNeg ? hR : hL, hF = isNeg ? hL : hR;
-                    const uint32_t wN = isNeg ? wR : wL, wF = isNeg ? wL : wR;
-                    const float loN = isNeg ? loR : loL, loF = isNeg ? loL : loR;
-                    if (hN && hF) {
-                        stack[64u * sp] = make_uint2(wF, __float_as_uint(loF));
+                    const ChildPair ch = cb_children(cnodes, cur, R, negMask, tMin, tMax);
+                    if (ch.hN && ch.hF) {
+                        stack[64u * sp] = make_uint2(ch.wF, __float_as_uint(ch.loF));
                         ++sp;
                     }
-                    if (hN || hF) {
-                        cur = hN ? wN : wF;
-                        curLo = hN ? loN : loF;
+                    if (ch.hN || ch.hF) {
+                        cur = ch.hN ? ch.wN : ch.wF;
+                        curLo = ch.hN ? ch.loN : ch.loF;
                     } else {
                         done = true;
                         while (sp > 0) {
@@ -1600,7 +1597,7 @@ PT_API int pt_set_scene(pt_context* ctx, const pt_bvh_node* nodes, uint32_t node
         q[0] = make_float4(L.aabb_min[0], L.aabb_max[0], L.aabb_min[1], L.aabb_max[1]);
         q[1] = make_float4(L.aabb_min[2], L.aabb_max[2], R.aabb_min[2], R.aabb_max[2]);
         q[2] = make_float4(R.aabb_min[0], R.aabb_max[0], R.aabb_min[1], R.aabb_max[1]);
-        q[3] = make_float4(u2f(word(i + 1)), u2f(word(nodes[i].offset)), u2f((nodes[i].primitive_count_axis >> 8) & 0xffu), 0.0f);
+        q[3] = make_float4(u2f(word(i + 1)), u2f(word(nodes[i].offset)), u2f(1u << ((nodes[i].primitive_count_axis >> 8) & 0xffu)), 0.0f);
     }
     for (uint32_t i = 0; i < prim_count; ++i) {
         const pt_hittable& h = prims[i];
