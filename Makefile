@@ -2,6 +2,7 @@
 #   pathtracercuda_amd/lib/libpt_hip.so   HIP kernels + device C ABI (include/pt_hip.h), gfx950
 #   pathtracercuda_amd/lib/libpt_host.so  host C++ layer + C ABI (include/pathtracer_amd.hpp, pt_host.h)
 #   pathtracercuda_amd/lib/pathtracer     CLI (reference main.cpp headless path)
+#   pathtracercuda_amd/lib/fp_exhaustive  all-inputs check of the kernel's fast 1/x and sqrt (GPU)
 #   oracle/liboracle.so                   CPU restatement (test infrastructure only)
 # Every FP unit is built with -ffp-contract=off: the GPU result is compared bit for bit with the
 # oracle, and the host-built BVH / transforms / camera feed the GPU directly.
@@ -20,7 +21,7 @@ HIPFLAGS ?= --offload-arch=$(ARCH) -O3 -std=c++17 -ffp-contract=off -fPIC -fvisi
 CXXFLAGS ?= -O2 -std=c++17 -ffp-contract=off -fno-fast-math -fPIC -Iinclude -I$(SRC)/host -Wall -Wextra \
             -Wno-unused-parameter -Wno-missing-field-initializers
 
-all: $(LIB)/libpt_hip.so $(LIB)/libpt_host.so $(LIB)/pathtracer oracle
+all: $(LIB)/libpt_hip.so $(LIB)/libpt_host.so $(LIB)/pathtracer $(LIB)/fp_exhaustive oracle
 
 $(LIB):
 	mkdir -p $(LIB)
@@ -33,6 +34,9 @@ $(LIB)/libpt_host.so: $(HOST_SRCS) $(HOST_HDRS) $(LIB)/libpt_hip.so
 
 $(LIB)/pathtracer: $(SRC)/host/cli_main.cpp $(LIB)/libpt_host.so
 	$(CXX) $(CXXFLAGS) -o $@ $(SRC)/host/cli_main.cpp -L$(LIB) -lpt_host -lpt_hip -lpthread -Wl,-rpath,'$$ORIGIN'
+
+$(LIB)/fp_exhaustive: tools/fp_exhaustive.hip $(SRC)/pt_math.h | $(LIB)
+	$(HIPCC) --offload-arch=$(ARCH) -O3 -std=c++17 -ffp-contract=off -o $@ tools/fp_exhaustive.hip
 
 oracle:
 	$(MAKE) -C oracle

@@ -148,7 +148,7 @@ PT_DEV bool quadric_roots(uint32_t type, const LocalRay& r, float& t0, float& t1
     // quadratic (Hittable.inl:7-39)
     const float disc = b * b - 4.0f * a * c;
     if (disc < 0.0f) return false;
-    const float rt = sqrtf(disc);
+    const float rt = sqrt_rn(disc);
     const float q = b < 0.0f ? -0.5f * (b - rt) : -0.5f * (b + rt);
     float x0 = q / a;
     float x1 = c / q;
@@ -185,7 +185,7 @@ PT_DEV bool prim_hit(const float4* __restrict__ prims, uint32_t p, f3 o, f3 d, f
         const float dx[3] = {r.d.x, r.d.y, r.d.z};
 #pragma unroll
         for (int a = 0; a < 3; ++a) {
-            const float invD = 1.0f / dx[a];
+            const float invD = rcp_rn(dx[a]);
             float t0 = (-1.0f - ox[a]) * invD;
             float t1 = (1.0f - ox[a]) * invD;
             if (invD < 0.0f) { const float tmp = t0; t0 = t1; t1 = tmp; }
@@ -311,7 +311,7 @@ PT_DEV uint32_t traverse(const float4* __restrict__ nodes, const float4* __restr
 {
     const float tMin = 0.001f;
     float tMax = kFltMax;
-    const float ix = 1.0f / d.x, iy = 1.0f / d.y, iz = 1.0f / d.z;
+    const float ix = rcp_rn(d.x), iy = rcp_rn(d.y), iz = rcp_rn(d.z);
     // trace.cu:31-36: dirIsNeg from 1/(d != 0 ? d : 1e-7) < 0, i.e. d < 0
     const uint32_t negMask = (d.x < 0.0f ? 1u : 0u) | (d.y < 0.0f ? 2u : 0u) | (d.z < 0.0f ? 4u : 0u);
     const bool fast = slabFast && __builtin_isfinite(ix) && __builtin_isfinite(iy) && __builtin_isfinite(iz);
@@ -487,9 +487,9 @@ PT_DEV uint32_t traverse_cb(const float4* __restrict__ cnodes, const float4* __r
     float tMax = kFltMax;
     SlabRay R;
     R.o = o;
-    R.ix = 1.0f / d.x;
-    R.iy = 1.0f / d.y;
-    R.iz = 1.0f / d.z;
+    R.ix = rcp_rn(d.x);
+    R.iy = rcp_rn(d.y);
+    R.iz = rcp_rn(d.z);
     R.fast = P.slabFast && __builtin_isfinite(R.ix) && __builtin_isfinite(R.iy) && __builtin_isfinite(R.iz);
     R.ox2 = f2(o.x, o.x);
     R.oy2 = f2(o.y, o.y);
@@ -568,9 +568,9 @@ PT_DEV bool traverse_cb_phase(const float4* __restrict__ cnodes, const float4* _
     const float tMin = 0.001f;
     SlabRay R;
     R.o = o;
-    R.ix = 1.0f / d.x;
-    R.iy = 1.0f / d.y;
-    R.iz = 1.0f / d.z;
+    R.ix = rcp_rn(d.x);
+    R.iy = rcp_rn(d.y);
+    R.iz = rcp_rn(d.z);
     R.fast = P.slabFast && __builtin_isfinite(R.ix) && __builtin_isfinite(R.iy) && __builtin_isfinite(R.iz);
     R.ox2 = f2(o.x, o.x);
     R.oy2 = f2(o.y, o.y);
@@ -662,9 +662,9 @@ PT_DEV uint32_t traverse_spec(const float4* __restrict__ cnodes, const float4* _
     float tMax = kFltMax;
     SlabRay R;
     R.o = o;
-    R.ix = 1.0f / d.x;
-    R.iy = 1.0f / d.y;
-    R.iz = 1.0f / d.z;
+    R.ix = rcp_rn(d.x);
+    R.iy = rcp_rn(d.y);
+    R.iz = rcp_rn(d.z);
     R.fast = P.slabFast && __builtin_isfinite(R.ix) && __builtin_isfinite(R.iy) && __builtin_isfinite(R.iz);
     R.ox2 = f2(o.x, o.x);
     R.oy2 = f2(o.y, o.y);
@@ -833,13 +833,13 @@ PT_DEV f3 vndf_sample_rsc(f3 V, float r, float s, float c, float a)
 {
     const f3 Vh = normalize(mk(a * V.x, a * V.y, V.z));
     const float lensq = Vh.x * Vh.x + Vh.y * Vh.y;
-    const f3 T1 = lensq > 0.0f ? scale(1.0f / sqrtf(lensq), mk(-Vh.y, Vh.x, 0.0f)) : mk(1.0f, 0.0f, 0.0f);
+    const f3 T1 = lensq > 0.0f ? scale(rcp_rn(sqrt_rn(lensq)), mk(-Vh.y, Vh.x, 0.0f)) : mk(1.0f, 0.0f, 0.0f);
     const f3 T2 = cross(Vh, T1);
     const float t1 = r * c;
     float t2 = r * s;
     const float sv = 0.5f * (1.0f + Vh.z);
-    t2 = (1.0f - sv) * sqrtf(1.0f - t1 * t1) + sv * t2;
-    const f3 Nh = add(add(scale(t1, T1), scale(t2, T2)), scale(sqrtf(clamp01(1.0f - t1 * t1 - t2 * t2)), Vh));
+    t2 = (1.0f - sv) * sqrt_rn(1.0f - t1 * t1) + sv * t2;
+    const f3 Nh = add(add(scale(t1, T1), scale(t2, T2)), scale(sqrt_rn(clamp01(1.0f - t1 * t1 - t2 * t2)), Vh));
     return normalize(mk(a * Nh.x, a * Nh.y, clamp01(Nh.z)));
 }
 
@@ -848,7 +848,7 @@ PT_DEV float vndf_pdf(f3 H, f3 V, float a)    // MonteCarlo.h:104-114
     const float a2 = a * a;
     const float NdotH = H.z;
     const float VdotH = clamp01(dot(V, H));
-    const float G1 = (2.0f * V.z) / (V.z + sqrtf(a2 + (1.0f - a2) * (V.z * V.z)));
+    const float G1 = (2.0f * V.z) / (V.z + sqrt_rn(a2 + (1.0f - a2) * (V.z * V.z)));
     const float Dv = (G1 * VdotH * d_ggx(NdotH, a2)) / V.z;
     return Dv / (4.0f * VdotH);
 }
@@ -856,8 +856,8 @@ PT_DEV float vndf_pdf(f3 H, f3 V, float a)    // MonteCarlo.h:104-114
 PT_DEV f3 specular_ggx(f3 F0, float NdotV, float NdotL, float NdotH, float VdotH, float a2)  // brdf.h:56-62
 {
     const float D = d_ggx(NdotH, a2);
-    const float lv = NdotL * sqrtf((-NdotV * a2 + NdotV) * NdotV + a2);   // brdf.h:18-24
-    const float ll = NdotV * sqrtf((-NdotL * a2 + NdotL) * NdotL + a2);
+    const float lv = NdotL * sqrt_rn((-NdotV * a2 + NdotV) * NdotV + a2);   // brdf.h:18-24
+    const float ll = NdotV * sqrt_rn((-NdotL * a2 + NdotL) * NdotL + a2);
     const float Vis = 0.5f / (lv + ll + 1e-5f);
     const float v = 1.0f - VdotH;                                          // brdf.h:27-32
     const float v2 = v * v;
@@ -953,16 +953,16 @@ PT_DEV bool shade(const TraceParams& P, const float4* __restrict__ prims, uint32
     }
     float sn, cs;
     sincos_pos(kTwoPi * (specular ? rnd1 : rnd0), sn, cs);
-    const float sq = sqrtf(specular ? rnd0 : rnd1);
+    const float sq = sqrt_rn(specular ? rnd0 : rnd1);
     if (mtype == 0u) {                                                        // LAMBERT (Material.inl:67-72)
-        dir = mk(cs * sqrtf(1.0f - rnd1), sn * sqrtf(1.0f - rnd1), sq);       // cosine_sample
+        dir = mk(cs * sqrt_rn(1.0f - rnd1), sn * sqrt_rn(1.0f - rnd1), sq);       // cosine_sample
         pdf = dir.z / kPi;
         att = scale(kInvPi, base);
     } else if (mtype <= 2u) {
         if (specular) {
             dir = reflect(neg(V), vndf_sample_rsc(V, sq, sn, cs, a));
         } else {
-            const float sinTheta = sqrtf(1.0f - rnd1);
+            const float sinTheta = sqrt_rn(1.0f - rnd1);
             dir = mk(cs * sinTheta, sn * sinTheta, sq);
         }
         if (dir.z < 0.0f) {
@@ -1197,9 +1197,9 @@ __global__ void __launch_bounds__(256, MINW) trace_sched_kernel(TraceParams P)
     bool fresh = true;   // a new ray needs its traversal set up
     while (true) {
         if (state == ST_NODE && fresh) {
-            ix = 1.0f / ps.d.x;
-            iy = 1.0f / ps.d.y;
-            iz = 1.0f / ps.d.z;
+            ix = rcp_rn(ps.d.x);
+            iy = rcp_rn(ps.d.y);
+            iz = rcp_rn(ps.d.z);
             negMask = (ps.d.x < 0.0f ? 1u : 0u) | (ps.d.y < 0.0f ? 2u : 0u) | (ps.d.z < 0.0f ? 4u : 0u);
             tMax = kFltMax;
             cur = 0;

@@ -122,6 +122,22 @@ def test_tile_schedule_does_not_change_results(gpu_available, scenes):
         assert_bitexact(sorted_acc, ref.accum, f"sorted schedule {W}x{H}")
 
 
+def test_fast_reciprocal_and_sqrt_exhaustive(gpu_available, root):
+    # pt::rcp_rn / pt::sqrt_rn (pt_math.h) against hipcc's correctly rounded 1.0f/x and sqrtf(x)
+    # for every one of the 2^32 float inputs
+    import json
+    import subprocess
+    exe = root / "pathtracercuda_amd" / "lib" / "fp_exhaustive"
+    out = subprocess.run([str(exe)], capture_output=True, text=True, timeout=300, check=True).stdout
+    res = json.loads(out)
+    assert res["inputs"] == 2 ** 32
+    assert res["rcp_rn"]["mismatches"] == 0, res["rcp_rn"]
+    assert res["sqrt_rn"]["mismatches"] == 0, res["sqrt_rn"]
+    # the guards matter: the raw sequences are not correctly rounded everywhere
+    assert res["diag_rcp_newton_unguarded"]["mismatches"] > 0
+    assert res["diag_sqrt_corrected_unguarded"]["mismatches"] > 0
+
+
 def test_history_semantics(gpu_available, scenes):
     # render(cam, spp, ignoreHistory) sequence: trace.cu:196 and Pathtracer.cpp:164-167,226
     pt, cam, ref, osc = pair(scenes / "test_shapes.scene.json", 48, 40)
