@@ -147,6 +147,9 @@ PT_API int pt_copy_accum_device(pt_context *ctx, void *dst_device, size_t bytes)
 /* tonemap kernel (tonemap.cu:4-27) over the local rows: accum / frames, Reinhard, gamma 2.2,
  * truncation to 8 bits, alpha 255 (RGBA8, rows x width). */
 PT_API int pt_tonemap(pt_context *ctx, uint32_t frames, uint8_t *dst);
+/* Same, into a device buffer of >= rows*width*4 bytes (RGBA8): the replacement of render()'s
+ * OpenGL pixel-buffer tonemap (Pathtracer.cpp:207-221) for a progressive viewer. */
+PT_API int pt_tonemap_device(pt_context *ctx, uint32_t frames, void *dst, size_t dst_bytes);
 
 /* Per-pixel XORWOW state (d, v0..v4 as uint32, rows x width x 6) -- for tests/checkpoints. */
 PT_API int pt_read_rng(pt_context *ctx, uint32_t *dst);
@@ -159,9 +162,10 @@ PT_API uint32_t pt_local_rows(const pt_context *ctx);
  * occupancy target).  All variants produce bit-identical results. */
 PT_API int pt_set_kernel_variant(pt_context *ctx, int variant);
 
-/* Tile dispatch order: 0 = by the measured cost of each 8x8 tile, most expensive first (default;
- * the first launch after a scene, texture or camera change records the costs in row-major
- * order), 1 = always row-major.  Results are identical; only the launch tail changes. */
+/* Tile dispatch order: 0 = by the measured cost of each 8x8 tile, most expensive first (default:
+ * every launch records the tile costs, and after a scene, texture or camera change the order is
+ * rebuilt on the device from the latest launch), 1 = always row-major.  Results are identical;
+ * only the launch tail changes. */
 PT_API int pt_set_schedule(pt_context *ctx, int mode);
 PT_API const char *pt_last_error(const pt_context *ctx);
 

@@ -43,6 +43,11 @@ PT_API int pth_scene_texture_data(const pth_scene *scene, uint32_t handle, float
 /* Camera ctor (Camera.inl:4-23, fovy in radians) and SceneLoader's degree conversion. */
 PT_API int pth_camera_make(const float *position, const float *lookat, const float *up, float fovy_radians, float aspect,
                            pt_camera *out);
+
+/* Camera::rotate / Camera::translate (Camera.inl:30-52) on a camera record, in place: the
+ * interactive controls of main.cpp:330-376 (the reference resets the accumulation after either). */
+PT_API int pth_camera_rotate(pt_camera *cam, float pitch, float yaw, float roll);
+PT_API int pth_camera_translate(pt_camera *cam, float x, float y, float z);
 PT_API float pth_radians(float degrees);
 
 /* Pathtracer on `device`, covering rows y = row_offset + k * row_stride. */

@@ -472,6 +472,42 @@ OR_EXPORT void or_camera_make(const float *position, const float *lookat, const 
     c->vertical = v3_scale(2.0f * hh, c->up);
 }
 
+/* Camera::rotate / translate / update (Camera.inl:30-62), rotateAroundVector (vec3.inl:184-187) */
+static v3 rotate_around(v3 v, v3 axis, float c, float s)
+{
+    return v3_add(v3_add(v3_scale(c, v), v3_scale(s, v3_cross(axis, v))),
+                  v3_scale(1.0f - c, v3_scale(v3_dot(axis, v), axis)));
+}
+
+static void camera_update(or_camera *c)
+{
+    float hh = c->tanHalfFovy;
+    float hw = c->aspectRatio * hh;
+    c->lowerLeftCorner = v3_sub(v3_add(v3_scale(-hw, c->right), v3_scale(-hh, c->up)), c->backward);
+    c->horizontal = v3_scale(2.0f * hw, c->right);
+    c->vertical = v3_scale(2.0f * hh, c->up);
+}
+
+OR_EXPORT void or_camera_rotate(or_camera *c, float pitch, float yaw, float roll)
+{
+    (void)roll;
+    const float cp = cosf(-pitch), sp = sinf(-pitch);
+    c->up = rotate_around(c->up, c->right, cp, sp);
+    c->backward = rotate_around(c->backward, c->right, cp, sp);
+    const float cy = cosf(-yaw), sy = sinf(-yaw);
+    const v3 Y = V(0.0f, 1.0f, 0.0f);
+    c->right = rotate_around(c->right, Y, cy, sy);
+    c->up = rotate_around(c->up, Y, cy, sy);
+    c->backward = rotate_around(c->backward, Y, cy, sy);
+    camera_update(c);
+}
+
+OR_EXPORT void or_camera_translate(or_camera *c, float x, float y, float z)
+{
+    c->origin = v3_add(c->origin, v3_add(v3_add(v3_scale(x, c->right), v3_scale(y, c->up)), v3_scale(z, c->backward)));
+    camera_update(c);
+}
+
 /* ------------------------------------------------------------------------------------------ */
 /* BVH build (BVH.cpp:5-15, 54-228) with libstdc++'s std::partition / std::nth_element        */
 /* ------------------------------------------------------------------------------------------ */

@@ -78,6 +78,8 @@ def lib() -> C.CDLL:
         L.or_cpu_hittable_make.argtypes = [C.c_uint32, P(f), P(f), P(f), P(Material), P(CpuHittable)]
         L.or_gpu_hittable.argtypes = [P(CpuHittable), P(Hittable)]
         L.or_camera_make.argtypes = [P(f), P(f), P(f), f, f, P(Camera)]
+        L.or_camera_rotate.argtypes = [P(Camera), f, f, f]
+        L.or_camera_translate.argtypes = [P(Camera), f, f, f]
         L.or_bvh_build.restype = C.c_uint32
         L.or_bvh_build.argtypes = [C.c_size_t, P(CpuHittable), C.c_uint32, P(BVHNode)]
         L.or_init_rand_state.argtypes = [C.c_uint32] * 4 + [P(Xorwow)]

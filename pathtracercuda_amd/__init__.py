@@ -24,7 +24,7 @@ import numpy as np
 from . import _native as N
 from ._native import PathtracerError, PtBvhNode, PtCamera, PtHittable, PtRenderStats, device_count
 
-__all__ = ["Pathtracer", "Scene", "make_camera", "radians", "device_count", "PathtracerError", "PtCamera",
+__all__ = ["Pathtracer", "Scene", "make_camera", "camera_rotate", "camera_translate", "radians", "device_count", "PathtracerError", "PtCamera",
            "PtBvhNode", "PtHittable", "write_png", "write_hdr", "HITTABLE_TYPES", "MATERIAL_TYPES"]
 
 HITTABLE_TYPES = ["SPHERE", "CYLINDER", "DISK", "CONE", "PARABOLOID", "QUAD", "CUBE"]   # Hittable.h:9-12
@@ -46,6 +46,18 @@ def make_camera(position, look_at, up=(0.0, 1.0, 0.0), fovy_radians: float = 1.0
     N.check_host(N.host().pth_camera_make(_f3(position), _f3(look_at), _f3(up), float(fovy_radians), float(aspect),
                                           C.byref(cam)))
     return cam
+
+
+def camera_rotate(camera: PtCamera, pitch: float, yaw: float, roll: float = 0.0) -> PtCamera:
+    """Camera::rotate (Camera.inl:30-45), in place; returns the camera."""
+    N.check_host(N.host().pth_camera_rotate(C.byref(camera), float(pitch), float(yaw), float(roll)))
+    return camera
+
+
+def camera_translate(camera: PtCamera, x: float, y: float, z: float) -> PtCamera:
+    """Camera::translate (Camera.inl:47-51), in place; returns the camera."""
+    N.check_host(N.host().pth_camera_translate(C.byref(camera), float(x), float(y), float(z)))
+    return camera
 
 
 def write_png(path: str, rgba: np.ndarray, flip: bool = True) -> None:
@@ -217,6 +229,11 @@ class Pathtracer:
 
     def copy_accum_to_device(self, dst_ptr: int, nbytes: int) -> None:
         N.check_ctx(N.hip().pt_copy_accum_device(self._ctx, C.c_void_p(int(dst_ptr)), int(nbytes)), self._ctx)
+
+    def tonemap_device(self, dst_ptr: int, nbytes: int, frames: Optional[int] = None) -> None:
+        """Tonemap into a device buffer (RGBA8, rows x width) -- the pixel-buffer path of render()."""
+        f = self.frames if frames is None else int(frames)
+        N.check_ctx(N.hip().pt_tonemap_device(self._ctx, f, C.c_void_p(int(dst_ptr)), int(nbytes)), self._ctx)
 
     def tonemap(self, frames: Optional[int] = None) -> np.ndarray:
         out = np.zeros((self.rows, self.width, 4), dtype=np.uint8)

@@ -61,6 +61,7 @@ _HIP_SYMBOLS = {
     "pt_read_accum": (C.c_int, [C.c_void_p, P(C.c_float)]),
     "pt_copy_accum_device": (C.c_int, [C.c_void_p, C.c_void_p, C.c_size_t]),
     "pt_tonemap": (C.c_int, [C.c_void_p, C.c_uint32, P(C.c_uint8)]),
+    "pt_tonemap_device": (C.c_int, [C.c_void_p, C.c_uint32, C.c_void_p, C.c_size_t]),
     "pt_read_rng": (C.c_int, [C.c_void_p, P(C.c_uint32)]),
     "pt_write_rng": (C.c_int, [C.c_void_p, P(C.c_uint32)]),
     "pt_local_rows": (C.c_uint32, [C.c_void_p]),
@@ -84,6 +85,8 @@ _HOST_SYMBOLS = {
     "pth_scene_texture_info": (C.c_int, [C.c_void_p, C.c_uint32, P(C.c_uint32), P(C.c_uint32)]),
     "pth_scene_texture_data": (C.c_int, [C.c_void_p, C.c_uint32, P(C.c_float)]),
     "pth_camera_make": (C.c_int, [P(C.c_float), P(C.c_float), P(C.c_float), C.c_float, C.c_float, P(PtCamera)]),
+    "pth_camera_rotate": (C.c_int, [P(PtCamera), C.c_float, C.c_float, C.c_float]),
+    "pth_camera_translate": (C.c_int, [P(PtCamera), C.c_float, C.c_float, C.c_float]),
     "pth_radians": (C.c_float, [C.c_float]),
     "pth_renderer_create": (C.c_int, [C.c_uint32, C.c_uint32, C.c_int, C.c_uint32, C.c_uint32, P(C.c_void_p)]),
     "pth_renderer_destroy": (None, [C.c_void_p]),

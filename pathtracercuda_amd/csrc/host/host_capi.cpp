@@ -155,6 +155,39 @@ PT_API int pth_camera_make(const float* position, const float* lookat, const flo
     return PT_OK;
 }
 
+static Camera camera_from_device(const pt_camera& d)
+{
+    Camera c(vec3(0.0f, 0.0f, 0.0f), vec3(0.0f, 0.0f, -1.0f), vec3(0.0f, 1.0f, 0.0f), 1.0f, 1.0f);
+    c.m_tanHalfFovy = d.tan_half_fovy;
+    c.m_aspectRatio = d.aspect_ratio;
+    c.m_origin = vec3(d.origin[0], d.origin[1], d.origin[2]);
+    c.m_lowerLeftCorner = vec3(d.lower_left_corner[0], d.lower_left_corner[1], d.lower_left_corner[2]);
+    c.m_horizontal = vec3(d.horizontal[0], d.horizontal[1], d.horizontal[2]);
+    c.m_vertical = vec3(d.vertical[0], d.vertical[1], d.vertical[2]);
+    c.m_right = vec3(d.right[0], d.right[1], d.right[2]);
+    c.m_up = vec3(d.up[0], d.up[1], d.up[2]);
+    c.m_backward = vec3(d.backward[0], d.backward[1], d.backward[2]);
+    return c;
+}
+
+PT_API int pth_camera_rotate(pt_camera* cam, float pitch, float yaw, float roll)
+{
+    if (!cam) return setError(PT_ERR_ARG, "invalid argument");
+    Camera c = camera_from_device(*cam);
+    c.rotate(pitch, yaw, roll);
+    *cam = c.toDevice();
+    return PT_OK;
+}
+
+PT_API int pth_camera_translate(pt_camera* cam, float x, float y, float z)
+{
+    if (!cam) return setError(PT_ERR_ARG, "invalid argument");
+    Camera c = camera_from_device(*cam);
+    c.translate(x, y, z);
+    *cam = c.toDevice();
+    return PT_OK;
+}
+
 PT_API float pth_radians(float degrees) { return ptamd::radians(degrees); }
 
 #define PTH_GUARD_BEGIN                      \

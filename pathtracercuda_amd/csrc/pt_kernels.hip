@@ -20,6 +20,7 @@
 //   * the BVH node test hoists the per-ray reciprocals (bit-identical to recomputing them) and the
 //     hit record is reconstructed once for the closest hit instead of for every candidate hit.
 #include <hip/hip_runtime.h>
+#include <rocprim/device/device_radix_sort.hpp>
 #include <stdint.h>
 #include <string.h>
 #include <stdio.h>
@@ -1328,8 +1329,14 @@ struct pt_context {
     // tile scheduling: per-tile cost of the last launch and the cost-sorted dispatch order
     uint32_t* tileCost = nullptr;
     uint32_t* order = nullptr;
+    uint32_t* sortKeys = nullptr; // radix-sort scratch: sorted costs, tile ids, temp storage
+    uint32_t* tileIds = nullptr;
+    void* sortTemp = nullptr;
+    size_t sortTempBytes = 0;
+    uchar4* ldr = nullptr;        // tonemap staging buffer (pt_tonemap)
     uint32_t orderTiles = 0;      // tiles the device buffers hold
-    bool orderValid = false;
+    bool orderValid = false;      // `order` holds a cost-sorted permutation
+    bool orderStale = true;       // rebuild it after the next launch (scene, texture or camera changed)
     int schedule = 0;             // 0 = cost-sorted tiles (default), 1 = row-major
     pt_camera lastCam = {};
     std::string err;
@@ -1512,6 +1519,10 @@ PT_API void pt_destroy(pt_context* ctx)
     (void)hipFree(ctx->cnodes);
     (void)hipFree(ctx->tileCost);
     (void)hipFree(ctx->order);
+    (void)hipFree(ctx->ldr);
+    (void)hipFree(ctx->sortKeys);
+    (void)hipFree(ctx->tileIds);
+    (void)hipFree(ctx->sortTemp);
     (void)hipFree(ctx->texTable);
     (void)hipFree(ctx->stats);
     for (auto& t : ctx->hostTex) (void)hipFree((void*)t.texels);
@@ -1629,7 +1640,7 @@ PT_API int pt_set_scene(pt_context* ctx, const pt_bvh_node* nodes, uint32_t node
         PT_HIP_CHECK(ctx, hipMemcpy(ctx->cnodes, hc.data(), hc.size() * sizeof(float4), hipMemcpyHostToDevice));
         ctx->cnodeCount = interior;
     }
-    ctx->orderValid = false;
+    ctx->orderStale = true;
     ctx->rootWord = word(0);
     for (int k = 0; k < 3; ++k) {
         ctx->rootBox[2 * k] = nodes[0].aabb_min[k];
@@ -1660,7 +1671,7 @@ PT_API int pt_set_texture(pt_context* ctx, uint32_t handle, const float* rgba, u
     t.texels = mem;
     t.width = width;
     t.height = height;
-    ctx->orderValid = false;
+    ctx->orderStale = true;
     PT_HIP_CHECK(ctx, hipMemcpy(ctx->texTable, ctx->hostTex, sizeof(ctx->hostTex), hipMemcpyHostToDevice));
     return PT_OK;
 }
@@ -1717,11 +1728,14 @@ static int render_impl(pt_context* ctx, const pt_camera* cam, uint32_t spp, uint
     P.rootWord = ctx->rootWord;
     for (int k = 0; k < 6; ++k) P.rootBox[k] = ctx->rootBox[k];
     // Tile scheduling: a pixel's samples are sequential (one XORWOW stream), so a tile is the
-    // smallest unit of work and tiles differ several-fold in cost (sky vs geometry).  The first
-    // launch for a scene/camera records every tile's cost; later launches dispatch tiles in
-    // descending cost, so the launch tail consists of cheap tiles and the waves of a workgroup
-    // (which hold the group's LDS until the last one ends) have similar lengths.  The order
-    // changes which wave renders a pixel, never how: results are identical.
+    // smallest unit of work, and tiles differ several-fold in cost (sky vs geometry).  Every
+    // launch records each tile's cycle count; after a scene, texture or camera change the
+    // dispatch order is rebuilt on the device from the latest costs (most expensive first, a
+    // stable radix sort), so
+    // the launch tail consists of cheap tiles and the waves of a workgroup (which hold the
+    // group's LDS until the last one ends) have similar lengths.  A camera move keeps using the
+    // previous order for one launch.  The order changes which wave renders a tile, never how:
+    // results are identical.
     const uint32_t tiles = P.tilesX * P.tilesY;
     if (ctx->orderTiles != tiles) {
         (void)hipFree(ctx->tileCost);
@@ -1732,15 +1746,32 @@ static int render_impl(pt_context* ctx, const pt_camera* cam, uint32_t spp, uint
         ctx->orderValid = false;
         PT_HIP_CHECK(ctx, hipMalloc(&ctx->tileCost, (size_t)tiles * sizeof(uint32_t)));
         PT_HIP_CHECK(ctx, hipMalloc(&ctx->order, ((size_t)tiles + 64) * sizeof(uint32_t)));
+        (void)hipFree(ctx->sortKeys);
+        (void)hipFree(ctx->tileIds);
+        (void)hipFree(ctx->sortTemp);
+        ctx->sortKeys = ctx->tileIds = nullptr;
+        ctx->sortTemp = nullptr;
+        PT_HIP_CHECK(ctx, hipMalloc(&ctx->sortKeys, (size_t)tiles * sizeof(uint32_t)));
+        PT_HIP_CHECK(ctx, hipMalloc(&ctx->tileIds, (size_t)tiles * sizeof(uint32_t)));
+        ctx->sortTempBytes = 0;
+        PT_HIP_CHECK(ctx, rocprim::radix_sort_pairs_desc(nullptr, ctx->sortTempBytes, ctx->tileCost, ctx->sortKeys,
+                                                         ctx->tileIds, ctx->order, tiles, 0, 32, ctx->stream));
+        PT_HIP_CHECK(ctx, hipMalloc(&ctx->sortTemp, ctx->sortTempBytes ? ctx->sortTempBytes : 4));
+        PT_HIP_CHECK(ctx, hipMemsetAsync(ctx->tileCost, 0, (size_t)tiles * sizeof(uint32_t), ctx->stream));
+        std::vector<uint32_t> ident((size_t)tiles + 64);              // slots past the last tile stay invalid
+        for (size_t i = 0; i < ident.size(); ++i) ident[i] = (uint32_t)i;
+        PT_HIP_CHECK(ctx, hipMemcpy(ctx->order, ident.data(), ident.size() * sizeof(uint32_t), hipMemcpyHostToDevice));
+        PT_HIP_CHECK(ctx, hipMemcpy(ctx->tileIds, ident.data(), (size_t)tiles * sizeof(uint32_t), hipMemcpyHostToDevice));
         ctx->orderTiles = tiles;
+        ctx->orderStale = true;
     }
     if (memcmp(&ctx->lastCam, cam, sizeof(pt_camera)) != 0) {
-        ctx->orderValid = false;
+        ctx->orderStale = true;
         ctx->lastCam = *cam;
     }
-    const bool record = ctx->schedule == 0 && !ctx->orderValid;
-    P.order = (ctx->schedule == 0 && ctx->orderValid) ? ctx->order : nullptr;
-    P.tileCost = record ? ctx->tileCost : nullptr;
+    const bool sorted = ctx->schedule == 0;
+    P.order = (sorted && ctx->orderValid) ? ctx->order : nullptr;
+    P.tileCost = sorted ? ctx->tileCost : nullptr;
     if (stats) PT_HIP_CHECK(ctx, hipMemsetAsync(ctx->stats, 0, 16 * sizeof(unsigned long long), ctx->stream));
     PT_HIP_CHECK(ctx, hipEventRecord(ctx->ev0, ctx->stream));
     const int variant = pick_variant(ctx);
@@ -1751,13 +1782,14 @@ static int render_impl(pt_context* ctx, const pt_camera* cam, uint32_t spp, uint
     float ms = 0.0f;
     PT_HIP_CHECK(ctx, hipEventElapsedTime(&ms, ctx->ev0, ctx->ev1));
     if (gpu_ms) *gpu_ms = ms;
-    if (record) {
-        std::vector<uint32_t> cost(tiles), order((size_t)tiles + 64);
-        PT_HIP_CHECK(ctx, hipMemcpy(cost.data(), ctx->tileCost, (size_t)tiles * sizeof(uint32_t), hipMemcpyDeviceToHost));
-        for (uint32_t i = 0; i < tiles + 64; ++i) order[i] = i;      // slots past the last tile stay invalid
-        std::stable_sort(order.begin(), order.begin() + tiles, [&](uint32_t a, uint32_t b) { return cost[a] > cost[b]; });
-        PT_HIP_CHECK(ctx, hipMemcpy(ctx->order, order.data(), order.size() * sizeof(uint32_t), hipMemcpyHostToDevice));
+    if (sorted && (ctx->orderStale || !ctx->orderValid)) {
+        // stable radix sort of (cost, tile) pairs, descending: deterministic, ties in tile order
+        size_t bytes = ctx->sortTempBytes;
+        PT_HIP_CHECK(ctx, rocprim::radix_sort_pairs_desc(ctx->sortTemp, bytes, ctx->tileCost, ctx->sortKeys, ctx->tileIds,
+                                                         ctx->order, tiles, 0, 32, ctx->stream));
+        PT_HIP_CHECK(ctx, hipStreamSynchronize(ctx->stream));
         ctx->orderValid = true;
+        ctx->orderStale = false;
     }
     if (stats) {
         unsigned long long h[16];
@@ -1785,7 +1817,7 @@ PT_API int pt_set_schedule(pt_context* ctx, int mode)
 {
     if (!ctx || mode < 0 || mode > 1) return PT_ERR_ARG;
     ctx->schedule = mode;
-    ctx->orderValid = false;
+    ctx->orderStale = true;
     return PT_OK;
 }
 
@@ -1822,20 +1854,31 @@ PT_API int pt_copy_accum_device(pt_context* ctx, void* dst_device, size_t bytes)
     return PT_OK;
 }
 
+PT_API int pt_tonemap_device(pt_context* ctx, uint32_t frames, void* dst, size_t dst_bytes)
+{
+    if (!ctx || !dst) return PT_ERR_ARG;
+    const size_t npix = (size_t)ctx->rows * ctx->width;
+    if (dst_bytes < npix * sizeof(uchar4)) return fail(ctx, PT_ERR_ARG, "pt_tonemap_device: destination too small");
+    PT_HIP_CHECK(ctx, hipSetDevice(ctx->device));
+    if (npix == 0) return PT_OK;
+    tonemap_kernel<<<(unsigned)((npix + 255) / 256), 256, 0, ctx->stream>>>(static_cast<uchar4*>(dst), ctx->accum, npix,
+                                                                             frames);
+    PT_HIP_CHECK(ctx, hipGetLastError());
+    PT_HIP_CHECK(ctx, hipStreamSynchronize(ctx->stream));
+    return PT_OK;
+}
+
 PT_API int pt_tonemap(pt_context* ctx, uint32_t frames, uint8_t* dst)
 {
     if (!ctx || !dst) return PT_ERR_ARG;
     PT_HIP_CHECK(ctx, hipSetDevice(ctx->device));
     const size_t npix = (size_t)ctx->rows * ctx->width;
     if (npix == 0) return PT_OK;
-    uchar4* out = nullptr;
-    PT_HIP_CHECK(ctx, hipMalloc(&out, npix * sizeof(uchar4)));
-    tonemap_kernel<<<(unsigned)((npix + 255) / 256), 256, 0, ctx->stream>>>(out, ctx->accum, npix, frames);
-    hipError_t e = hipGetLastError();
-    if (e == hipSuccess) e = hipMemcpyAsync(dst, out, npix * sizeof(uchar4), hipMemcpyDeviceToHost, ctx->stream);
-    if (e == hipSuccess) e = hipStreamSynchronize(ctx->stream);
-    (void)hipFree(out);
-    PT_HIP_CHECK(ctx, e);
+    if (!ctx->ldr) PT_HIP_CHECK(ctx, hipMalloc(&ctx->ldr, npix * sizeof(uchar4)));   // kept for per-frame use
+    tonemap_kernel<<<(unsigned)((npix + 255) / 256), 256, 0, ctx->stream>>>(ctx->ldr, ctx->accum, npix, frames);
+    PT_HIP_CHECK(ctx, hipGetLastError());
+    PT_HIP_CHECK(ctx, hipMemcpyAsync(dst, ctx->ldr, npix * sizeof(uchar4), hipMemcpyDeviceToHost, ctx->stream));
+    PT_HIP_CHECK(ctx, hipStreamSynchronize(ctx->stream));
     return PT_OK;
 }
 

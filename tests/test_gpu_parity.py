@@ -138,6 +138,37 @@ def test_fast_reciprocal_and_sqrt_exhaustive(gpu_available, root):
     assert res["diag_sqrt_corrected_unguarded"]["mismatches"] > 0
 
 
+def test_progressive_frames_with_camera_moves(gpu_available, scenes):
+    # the windowed loop's call pattern (main.cpp:298-437): render(cam, 1, reset) per frame, a
+    # tonemap into a device pixel buffer every frame (Pathtracer.cpp:207-221), camera rotate /
+    # translate resetting the accumulation
+    import ctypes as C
+    import torch
+    W, H = 48, 32
+    pt, cam, ref, osc = pair(scenes / "generated_scene.scene.json", W, H)
+    L = po.lib()
+    ocam = po.Camera.from_buffer_copy(bytes(osc.camera))
+    dev = torch.empty((H, W, 4), dtype=torch.uint8, device="cuda:0")
+    reset = True
+    for frame in range(9):
+        if frame == 3:
+            pa.camera_rotate(cam, 0.05, -0.1, 0.0)
+            L.or_camera_rotate(C.byref(ocam), 0.05, -0.1, 0.0)
+            reset = True
+        if frame == 6:
+            pa.camera_translate(cam, 0.5, 0.0, -1.5)
+            L.or_camera_translate(C.byref(ocam), 0.5, 0.0, -1.5)
+            reset = True
+        assert bytes(cam) == bytes(ocam)
+        pt.render(cam, 1, reset)
+        ref.render(ocam, 1, reset)
+        reset = False
+        pt.tonemap_device(dev.data_ptr(), dev.numel())
+        assert pt.frames == ref.frames
+        assert np.array_equal(dev.cpu().numpy(), ref.tonemap()), f"frame {frame}"
+        assert_bitexact(pt.accum(), ref.accum, f"frame {frame}")
+
+
 def test_history_semantics(gpu_available, scenes):
     # render(cam, spp, ignoreHistory) sequence: trace.cu:196 and Pathtracer.cpp:164-167,226
     pt, cam, ref, osc = pair(scenes / "test_shapes.scene.json", 48, 40)

@@ -167,6 +167,27 @@ def test_png_and_hdr_writers(tmp_path):
     assert (np.abs(back[..., :3] - hdr[..., :3]) <= tol).all()
 
 
+def test_camera_rotate_translate_match_oracle():
+    # Camera::rotate / translate (Camera.inl:30-52): the interactive controls' camera updates
+    L = po.lib()
+    c = pa.make_camera((13, 2, 3), (0, 0, 0), fovy_radians=pa.radians(60.0), aspect=float(np.float32(16 / 9)))
+    o = po.Camera.from_buffer_copy(bytes(c))
+    rng = np.random.default_rng(7)
+    for step in range(40):
+        if step % 3 == 0:
+            x, y, z = (float(np.float32(v)) for v in rng.normal(0, 2, 3))
+            pa.camera_translate(c, x, y, z)
+            L.or_camera_translate(C.byref(o), x, y, z)
+        else:
+            p, yw = (float(np.float32(v)) for v in rng.normal(0, 0.3, 2))
+            pa.camera_rotate(c, p, yw, 0.0)
+            L.or_camera_rotate(C.byref(o), p, yw, 0.0)
+        assert bytes(c) == bytes(o), f"step {step}"
+    # the basis stays orthonormal to float accuracy
+    r, u, b = (np.array(getattr(c, k)) for k in ("right", "up", "backward"))
+    assert abs(np.dot(r, u)) < 1e-4 and abs(np.linalg.norm(b) - 1) < 1e-4
+
+
 def test_camera_matches_oracle():
     L = po.lib()
     for pos, look, fovy, aspect in [((13, 2, 3), (0, 0, 0), 60.0, 16 / 9), ((0, 1, 4), (0, 1, 0), 40.0, 1.0)]:
