@@ -17,6 +17,7 @@
 #pragma once
 
 #include <cstddef>
+#include <atomic>
 #include <cstdint>
 #include <string>
 #include <vector>
@@ -161,7 +162,8 @@ private:
     uint32_t m_maxLeafElements = 1;
     std::vector<BVHNode> m_nodes;
     std::vector<CpuHittable> m_elements;
-    uint32_t buildRecursive(size_t begin, size_t end);
+    uint32_t buildInto(std::vector<BVHNode>& out, size_t begin, size_t end);
+    std::atomic<int>* m_spareThreads = nullptr;   // worker-thread budget during build()
     bool validateRecursive(uint32_t node, std::vector<char>& reached);
 };
 

@@ -27,6 +27,10 @@ PT_API const char *pth_last_error(void);
  * textures decoded on the host (handle = load order, failures get handle 0 and no slot). */
 PT_API int pth_scene_load(const char *path, uint32_t width, uint32_t height, pth_scene **out);
 PT_API void pth_scene_free(pth_scene *scene);
+
+/* Host-side wall time of the load: JSON parse + transforms (SceneLoader.cpp:124-348) and the SAH
+ * BVH build (BVH.cpp:66-228; multi-threaded over independent subtrees, identical layout). */
+PT_API int pth_scene_timing(const pth_scene *scene, double *parse_ms, double *bvh_ms);
 PT_API uint32_t pth_scene_object_count(const pth_scene *scene);
 PT_API uint32_t pth_scene_node_count(const pth_scene *scene);
 PT_API uint32_t pth_scene_bvh_depth(const pth_scene *scene);

@@ -86,6 +86,12 @@ class Scene:
             N.host().pth_scene_free(h)
             self._h = None
 
+    def timing(self) -> Dict[str, float]:
+        """Host wall time of the load: {"parse_ms": JSON + transforms, "bvh_ms": SAH build}."""
+        a, b = C.c_double(), C.c_double()
+        N.check_host(N.host().pth_scene_timing(self._h, C.byref(a), C.byref(b)))
+        return {"parse_ms": a.value, "bvh_ms": b.value}
+
     @property
     def object_count(self) -> int:
         return int(N.host().pth_scene_object_count(self._h))

@@ -74,6 +74,7 @@ _HOST_SYMBOLS = {
     "pth_last_error": (C.c_char_p, []),
     "pth_scene_load": (C.c_int, [C.c_char_p, C.c_uint32, C.c_uint32, P(C.c_void_p)]),
     "pth_scene_free": (None, [C.c_void_p]),
+    "pth_scene_timing": (C.c_int, [C.c_void_p, P(C.c_double), P(C.c_double)]),
     "pth_scene_object_count": (C.c_uint32, [C.c_void_p]),
     "pth_scene_node_count": (C.c_uint32, [C.c_void_p]),
     "pth_scene_bvh_depth": (C.c_uint32, [C.c_void_p]),

@@ -6,8 +6,12 @@
 #include <algorithm>
 #include <cfloat>
 #include <climits>
+#include <cstdlib>
+#include <atomic>
 #include <cstring>
+#include <future>
 #include <limits>
+#include <thread>
 
 #include "pathtracer_amd.hpp"
 
@@ -38,7 +42,26 @@ void BVH::build(size_t elementCount, const CpuHittable* elements, uint32_t maxLe
     m_elements.assign(elements, elements + elementCount);
     if (elementCount == 0) return;
     m_nodes.reserve(2 * elementCount - 1);
-    buildRecursive(0, elementCount);
+    // Subtrees are independent (disjoint element ranges, per-node arithmetic only), so large
+    // subtrees build on worker threads into their own node arrays, which are then concatenated in
+    // depth-first order with interior offsets rebased: the result is the sequential layout exactly.
+    // (SAH splits can be very uneven, so threads go to nodes whose *smaller* side is large.)
+    unsigned hw = std::max(1u, std::thread::hardware_concurrency());
+    if (const char* env = getenv("PT_BVH_THREADS")) hw = std::max(1, atoi(env));   // 1 = sequential
+    std::atomic<int> spare((int)std::min(hw, 64u) - 1);
+    m_spareThreads = &spare;
+    buildInto(m_nodes, 0, elementCount);
+    m_spareThreads = nullptr;
+}
+
+// Appends a subtree built into its own array (root at index 0) at the end of `out`.
+static void appendSubtree(std::vector<BVHNode>& out, const std::vector<BVHNode>& sub)
+{
+    const uint32_t base = static_cast<uint32_t>(out.size());
+    for (BVHNode n : sub) {
+        if ((n.m_primitiveCountAxis >> 16) == 0) n.m_offset += base;   // interior: node index; leaf: element index
+        out.push_back(n);
+    }
 }
 
 uint32_t BVH::getDepth(uint32_t node) const
@@ -84,10 +107,10 @@ bool BVH::validateRecursive(uint32_t node, std::vector<char>& reached)
     return validateRecursive(node + 1, reached) && validateRecursive(m_nodes[node].m_offset, reached);
 }
 
-uint32_t BVH::buildRecursive(size_t begin, size_t end)
+uint32_t BVH::buildInto(std::vector<BVHNode>& out, size_t begin, size_t end)
 {
-    const uint32_t nodeIndex = static_cast<uint32_t>(m_nodes.size());
-    m_nodes.push_back({});
+    const uint32_t nodeIndex = static_cast<uint32_t>(out.size());
+    out.push_back({});
     BVHNode node = {};
     node.m_aabb.m_min = vec3(std::numeric_limits<float>::max());
     node.m_aabb.m_max = vec3(std::numeric_limits<float>::lowest());
@@ -162,13 +185,34 @@ uint32_t BVH::buildRecursive(size_t begin, size_t end)
                                  return lc[ax] < rc[ax];
                              });
         }
-        buildRecursive(begin, split);
-        node.m_offset = buildRecursive(split, end);
+        bool spawn = false;
+        if (m_spareThreads && std::min(split - begin, end - split) >= 4096) {
+            spawn = m_spareThreads->fetch_sub(1) > 0;
+            if (!spawn) m_spareThreads->fetch_add(1);
+        }
+        if (spawn) {
+            std::vector<BVHNode> left;
+            left.reserve(2 * (split - begin));
+            auto job = std::async(std::launch::async, [&] {
+                buildInto(left, begin, split);
+                m_spareThreads->fetch_add(1);
+            });
+            std::vector<BVHNode> right;
+            right.reserve(2 * (end - split));
+            buildInto(right, split, end);
+            job.get();
+            appendSubtree(out, left);                    // left child = nodeIndex + 1
+            node.m_offset = static_cast<uint32_t>(out.size());
+            appendSubtree(out, right);
+        } else {
+            buildInto(out, begin, split);
+            node.m_offset = buildInto(out, split, end);
+        }
         node.m_primitiveCountAxis |= (bestAxis << 8);
     } else {
         node.m_offset = static_cast<uint32_t>(begin);
         node.m_primitiveCountAxis |= static_cast<uint32_t>(end - begin) << 16;
     }
-    m_nodes[nodeIndex] = node;
+    out[nodeIndex] = node;
     return nodeIndex;
 }

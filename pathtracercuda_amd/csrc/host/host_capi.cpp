@@ -1,4 +1,5 @@
 // C ABI of the host layer (include/pt_host.h).
+#include <chrono>
 #include <cstring>
 #include <memory>
 #include <string>
@@ -31,6 +32,7 @@ struct pth_scene {
     std::vector<HostTexture> textures;
     std::string path;
     pt_camera camera;
+    double parseMs = 0.0, bvhMs = 0.0;
 };
 
 struct pth_renderer {
@@ -71,11 +73,16 @@ PT_API int pth_scene_load(const char* path, uint32_t width, uint32_t height, pth
     auto s = std::make_unique<pth_scene>();
     s->path = path;
     std::string err;
+    using clk = std::chrono::steady_clock;
+    const auto t0 = clk::now();
     if (!ptamd::parseSceneFile(path, s->desc, err, hostTextureLoader, s.get())) return setError(PT_ERR_ARG, err);
+    const auto t1 = clk::now();
     if (!s->desc.objects.empty()) {
         s->bvh.build(s->desc.objects.size(), s->desc.objects.data(), 4);
+        s->bvhMs = std::chrono::duration<double, std::milli>(clk::now() - t1).count();
         if (!s->bvh.validate()) return setError(PT_ERR_STATE, "BVH validation failed");
     }
+    s->parseMs = std::chrono::duration<double, std::milli>(t1 - t0).count();
     const Camera cam(s->desc.cameraPosition, s->desc.cameraLookAt, vec3(0.0f, 1.0f, 0.0f),
                      ptamd::radians(s->desc.cameraFovyDegrees), (float)width / height);
     s->camera = cam.toDevice();
@@ -84,6 +91,14 @@ PT_API int pth_scene_load(const char* path, uint32_t width, uint32_t height, pth
 }
 
 PT_API void pth_scene_free(pth_scene* scene) { delete scene; }
+
+PT_API int pth_scene_timing(const pth_scene* s, double* parse_ms, double* bvh_ms)
+{
+    if (!s) return setError(PT_ERR_ARG, "null scene");
+    if (parse_ms) *parse_ms = s->parseMs;
+    if (bvh_ms) *bvh_ms = s->bvhMs;
+    return PT_OK;
+}
 
 PT_API uint32_t pth_scene_object_count(const pth_scene* s) { return s ? (uint32_t)s->desc.objects.size() : 0; }
 PT_API uint32_t pth_scene_node_count(const pth_scene* s) { return s ? (uint32_t)s->bvh.getNodes().size() : 0; }

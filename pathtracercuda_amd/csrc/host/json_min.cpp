@@ -1,7 +1,7 @@
-// Recursive-descent JSON parser (RFC 8259) for the scene loader.
+// Recursive-descent JSON parser (RFC 8259) building a flat Document (json_min.h).
 #include "json_min.h"
 
-#include <cerrno>
+#include <charconv>
 #include <cstdio>
 #include <cstdlib>
 
@@ -9,10 +9,16 @@ namespace ptamd {
 namespace json {
 namespace {
 
+struct Child {
+    uint32_t node, keyA, keyN;
+};
+
 struct Parser {
     const char* p;
     const char* begin;
     const char* end;
+    Document& d;
+    std::vector<Child> scratch;     // children of the containers being parsed (a stack of ranges)
     std::string err;
     int depth = 0;
 
@@ -41,8 +47,9 @@ struct Parser {
         p = q;
         return true;
     }
-    static void utf8(std::string& o, uint32_t cp)
+    void utf8(uint32_t cp)
     {
+        std::string& o = d.strings;
         if (cp < 0x80) o += (char)cp;
         else if (cp < 0x800) { o += (char)(0xC0 | (cp >> 6)); o += (char)(0x80 | (cp & 0x3F)); }
         else if (cp < 0x10000) {
@@ -66,27 +73,31 @@ struct Parser {
         }
         return true;
     }
-    bool str(std::string& o)
+    // Appends the unescaped string to the arena; returns its (offset, length).
+    bool str(uint32_t& a, uint32_t& n)
     {
         if (p >= end || *p != '"') return fail("expected string");
         ++p;
+        a = (uint32_t)d.strings.size();
         while (true) {
+            const char* run = p;                           // copy escape-free runs in one go
+            while (p < end && *p != '"' && *p != '\\' && (unsigned char)*p >= 0x20) ++p;
+            d.strings.append(run, (size_t)(p - run));
             if (p >= end) return fail("unterminated string");
-            unsigned char c = (unsigned char)*p++;
-            if (c == '"') return true;
+            const unsigned char c = (unsigned char)*p++;
+            if (c == '"') break;
             if (c < 0x20) return fail("control character in string");
-            if (c != '\\') { o += (char)c; continue; }
             if (p >= end) return fail("unterminated escape");
-            char e = *p++;
+            const char e = *p++;
             switch (e) {
-            case '"': o += '"'; break;
-            case '\\': o += '\\'; break;
-            case '/': o += '/'; break;
-            case 'b': o += '\b'; break;
-            case 'f': o += '\f'; break;
-            case 'n': o += '\n'; break;
-            case 'r': o += '\r'; break;
-            case 't': o += '\t'; break;
+            case '"': d.strings += '"'; break;
+            case '\\': d.strings += '\\'; break;
+            case '/': d.strings += '/'; break;
+            case 'b': d.strings += '\b'; break;
+            case 'f': d.strings += '\f'; break;
+            case 'n': d.strings += '\n'; break;
+            case 'r': d.strings += '\r'; break;
+            case 't': d.strings += '\t'; break;
             case 'u': {
                 uint32_t cp;
                 if (!hex4(cp)) return false;
@@ -97,14 +108,16 @@ struct Parser {
                 } else if (cp >= 0xDC00 && cp <= 0xDFFF) {
                     return fail("invalid surrogate");
                 }
-                utf8(o, cp);
+                utf8(cp);
                 break;
             }
             default: return fail("invalid escape");
             }
         }
+        n = (uint32_t)(d.strings.size() - a);
+        return true;
     }
-    bool num(Value& v)
+    bool num(Node& v)
     {
         const char* s = p;
         bool isFloat = false;
@@ -126,86 +139,104 @@ struct Parser {
             if (p >= end || !(*p >= '0' && *p <= '9')) return fail("invalid number");
             while (p < end && *p >= '0' && *p <= '9') ++p;
         }
-        std::string tok(s, p);
         if (!isFloat) {
-            errno = 0;
-            char* e = nullptr;
-            long long iv = strtoll(tok.c_str(), &e, 10);
-            if (errno == 0 && e && *e == 0) {
-                v.kind = Value::Int;
+            int64_t iv = 0;
+            const auto r = std::from_chars(s, p, iv);
+            if (r.ec == std::errc() && r.ptr == p) {
+                v.kind = Kind::Int;
                 v.i = iv;
                 return true;
             }
-            // out of int64 range: nlohmann stores it as a float value (still an integer token)
+            uint64_t uv = 0;
+            const auto ru = std::from_chars(s, p, uv);
+            if (ru.ec == std::errc() && ru.ptr == p) {
+                v.kind = Kind::UInt;
+                v.u = uv;
+                return true;
+            }
+            // beyond uint64: nlohmann stores it as a float value (still an integer token)
         }
-        v.kind = Value::Float;
-        v.f = strtod(tok.c_str(), nullptr);
+        double fv = 0.0;
+        const auto r = std::from_chars(s, p, fv);          // correctly rounded, like strtod
+        if (r.ec == std::errc::result_out_of_range) fv = strtod(std::string(s, p).c_str(), nullptr);   // +-inf / 0
+        v.kind = Kind::Float;
+        v.f = fv;
         return true;
     }
-    bool value(Value& v)
+    bool value(uint32_t idx)
     {
         if (++depth > 512) return fail("nesting too deep");
         ws();
         if (p >= end) return fail("unexpected end of input");
-        bool ok;
+        bool ok = true;
         switch (*p) {
-        case '{': {
-            ++p;
-            v.kind = Value::Object;
-            ws();
-            if (p < end && *p == '}') { ++p; ok = true; break; }
-            ok = true;
-            while (true) {
-                ws();
-                std::string key;
-                if (!str(key)) { ok = false; break; }
-                ws();
-                if (p >= end || *p != ':') { ok = fail("expected ':'"); break; }
-                ++p;
-                Value child;
-                if (!value(child)) { ok = false; break; }
-                v.obj[key] = std::move(child);
-                ws();
-                if (p < end && *p == ',') { ++p; continue; }
-                if (p < end && *p == '}') { ++p; break; }
-                ok = fail("expected ',' or '}'");
-                break;
-            }
-            break;
-        }
+        case '{':
         case '[': {
+            const bool isObj = *p == '{';
+            const char close = isObj ? '}' : ']';
             ++p;
-            v.kind = Value::Array;
+            d.nodes[idx].kind = isObj ? Kind::Object : Kind::Array;
+            const size_t first = scratch.size();
             ws();
-            if (p < end && *p == ']') { ++p; ok = true; break; }
-            ok = true;
+            if (p < end && *p == close) { ++p; break; }
             while (true) {
-                Value child;
-                if (!value(child)) { ok = false; break; }
-                v.arr.push_back(std::move(child));
+                Child c{0, 0, 0};
+                if (isObj) {
+                    ws();
+                    if (!str(c.keyA, c.keyN)) { ok = false; break; }
+                    ws();
+                    if (p >= end || *p != ':') { ok = fail("expected ':'"); break; }
+                    ++p;
+                }
+                c.node = (uint32_t)d.nodes.size();
+                d.nodes.emplace_back();
+                if (!value(c.node)) { ok = false; break; }
+                scratch.push_back(c);
                 ws();
                 if (p < end && *p == ',') { ++p; continue; }
-                if (p < end && *p == ']') { ++p; break; }
-                ok = fail("expected ',' or ']'");
+                if (p < end && *p == close) { ++p; break; }
+                ok = fail(isObj ? "expected ',' or '}'" : "expected ',' or ']'");
                 break;
             }
+            if (ok) {
+                Node& n = d.nodes[idx];
+                n.a = (uint32_t)d.kids.size();
+                n.n = (uint32_t)(scratch.size() - first);
+                for (size_t k = first; k < scratch.size(); ++k) {
+                    d.kids.push_back(scratch[k].node);
+                    d.keyA.push_back(scratch[k].keyA);
+                    d.keyN.push_back(scratch[k].keyN);
+                }
+            }
+            scratch.resize(first);
             break;
         }
-        case '"':
-            v.kind = Value::String;
-            ok = str(v.s);
+        case '"': {
+            uint32_t a = 0, n = 0;
+            ok = str(a, n);
+            Node& v = d.nodes[idx];
+            v.kind = Kind::String;
+            v.a = a;
+            v.n = n;
             break;
+        }
         case 't':
-            ok = lit("true") ? (v.kind = Value::Bool, v.b = true, true) : fail("invalid literal");
+            if (lit("true")) { d.nodes[idx].kind = Kind::Bool; d.nodes[idx].b = true; }
+            else ok = fail("invalid literal");
             break;
         case 'f':
-            ok = lit("false") ? (v.kind = Value::Bool, v.b = false, true) : fail("invalid literal");
+            if (lit("false")) { d.nodes[idx].kind = Kind::Bool; d.nodes[idx].b = false; }
+            else ok = fail("invalid literal");
             break;
         case 'n':
-            ok = lit("null") ? (v.kind = Value::Null, true) : fail("invalid literal");
+            if (lit("null")) d.nodes[idx].kind = Kind::Null;
+            else ok = fail("invalid literal");
             break;
-        default:
+        default: {
+            Node v;
             ok = num(v);
+            d.nodes[idx] = v;
+        }
         }
         --depth;
         return ok;
@@ -214,14 +245,19 @@ struct Parser {
 
 } // namespace
 
-bool parse(const std::string& text, Value& out, std::string& error)
+bool parse(std::string_view text, Document& out, std::string& error)
 {
-    Parser ps{text.data(), text.data(), text.data() + text.size(), {}};
+    out = Document();
+    out.nodes.reserve(text.size() / 8 + 16);
+    out.kids.reserve(text.size() / 8 + 16);
+    out.keyA.reserve(text.size() / 8 + 16);
+    out.keyN.reserve(text.size() / 8 + 16);
+    Parser ps{text.data(), text.data(), text.data() + text.size(), out, {}, {}};
     // skip a UTF-8 BOM like nlohmann does
     if (text.size() >= 3 && (unsigned char)text[0] == 0xEF && (unsigned char)text[1] == 0xBB && (unsigned char)text[2] == 0xBF)
         ps.p += 3;
-    out = Value();
-    if (!ps.value(out)) { error = ps.err; return false; }
+    out.nodes.emplace_back();
+    if (!ps.value(0)) { error = ps.err; return false; }
     ps.ws();
     if (ps.p != ps.end) { ps.fail("unexpected trailing characters"); error = ps.err; return false; }
     return true;

@@ -12,39 +12,40 @@
 namespace ptamd {
 namespace {
 
+using json::Kind;
 using json::Value;
 
 bool getString(const Value& o, const char* key, std::string& out)
 {
-    const Value* v = o.get(key);
-    if (v && v->kind == Value::String) { out = v->s; return true; }
+    const Value v = o.get(key);
+    if (v.kind() == Kind::String) { out = std::string(v.str()); return true; }
     return false;
 }
 
 bool getFloat(const Value& o, const char* key, float& out)      // only JSON floats (is_number_float)
 {
-    const Value* v = o.get(key);
-    if (v && v->isFloat()) { out = (float)v->f; return true; }
+    const Value v = o.get(key);
+    if (v.isFloat()) { out = (float)v.f(); return true; }
     return false;
 }
 
 bool getVec3(const Value& o, const char* key, vec3& out)
 {
-    const Value* v = o.get(key);
-    if (v && v->kind == Value::Array && v->arr.size() == 3) {
+    const Value v = o.get(key);
+    if (v.kind() == Kind::Array && v.size() == 3) {
         // get<float>() on a non-number throws in nlohmann; treat such a file as malformed here
-        for (const Value& c : v->arr)
-            if (!c.isNumber()) return false;
-        out = vec3(v->arr[0].asFloat(), v->arr[1].asFloat(), v->arr[2].asFloat());
+        for (uint32_t k = 0; k < 3; ++k)
+            if (!v.at(k).isNumber()) return false;
+        out = vec3(v.at(0).asFloat(), v.at(1).asFloat(), v.at(2).asFloat());
         return true;
     }
     return false;
 }
 
-const Value* getObject(const Value& o, const char* key)
+Value getObject(const Value& o, const char* key)
 {
-    const Value* v = o.get(key);
-    return (v && v->kind == Value::Object) ? v : nullptr;
+    const Value v = o.get(key);
+    return v.kind() == Kind::Object ? v : Value();
 }
 
 } // namespace
@@ -57,10 +58,18 @@ bool parseSceneFile(const std::string& path, SceneDesc& out, std::string& error,
         error = "Failed to open input file: " + path;
         return false;
     }
-    std::stringstream ss;
-    ss << file.rdbuf();
-    Value root;
-    if (!json::parse(ss.str(), root, error)) return false;
+    std::string text;
+    file.seekg(0, std::ios::end);
+    const std::streamoff size = file.tellg();
+    file.seekg(0, std::ios::beg);
+    if (size > 0) {
+        text.resize((size_t)size);
+        file.read(&text[0], size);
+        text.resize((size_t)file.gcount());
+    }
+    json::Document doc;
+    if (!json::parse(text, doc, error)) return false;
+    const Value root = json::root(doc);
 
     out = SceneDesc();
     std::map<std::string, uint32_t> handles;
@@ -77,11 +86,12 @@ bool parseSceneFile(const std::string& path, SceneDesc& out, std::string& error,
         return h;
     };
 
-    const Value* objs = root.get("objects");
-    if (objs && objs->kind == Value::Array) {
+    const Value objs = root.get("objects");
+    if (objs.kind() == Kind::Array) {
         out.hasObjects = true;
-        out.objects.reserve(objs->arr.size());
-        for (const Value& o : objs->arr) {
+        out.objects.reserve(objs.size());
+        for (uint32_t oi = 0; oi < objs.size(); ++oi) {
+            const Value o = objs.at(oi);
             HittableType htype = HittableType::SPHERE;
             vec3 position = 0.0f, rotation = 0.0f, scale = 1.0f;
             MaterialType mtype = MaterialType::LAMBERT;
@@ -99,20 +109,20 @@ bool parseSceneFile(const std::string& path, SceneDesc& out, std::string& error,
             getVec3(o, "position", position);
             getVec3(o, "rotation", rotation);
             getVec3(o, "scale", scale);
-            if (const Value* m = getObject(o, "material")) {
+            if (const Value m = getObject(o, "material"); m.valid()) {
                 std::string mt;
-                if (getString(*m, "type", mt)) {
+                if (getString(m, "type", mt)) {
                     if (mt == "LAMBERT") mtype = MaterialType::LAMBERT;
                     else if (mt == "GGX") mtype = MaterialType::GGX;
                     else if (mt == "LAMBERT_GGX") mtype = MaterialType::LAMBERT_GGX;
                     else { printf("Failed to parse material type: %s\n", mt.c_str()); fflush(stdout); }
                 }
-                getVec3(*m, "baseColor", baseColor);
-                getVec3(*m, "emissive", emissive);
-                getFloat(*m, "roughness", roughness);
-                getFloat(*m, "metalness", metalness);
+                getVec3(m, "baseColor", baseColor);
+                getVec3(m, "emissive", emissive);
+                getFloat(m, "roughness", roughness);
+                getFloat(m, "metalness", metalness);
                 std::string tp;
-                if (getString(*m, "texture", tp)) tex = textureHandle(tp);
+                if (getString(m, "texture", tp)) tex = textureHandle(tp);
             }
             out.objects.push_back(CpuHittable(htype, position,
                                               vec3(radians(rotation.x), radians(rotation.y), radians(rotation.z)), scale,
@@ -124,10 +134,10 @@ bool parseSceneFile(const std::string& path, SceneDesc& out, std::string& error,
         out.hasSkybox = true;
         out.skyboxHandle = textureHandle(sky);
     }
-    if (const Value* c = getObject(root, "camera")) {
-        getVec3(*c, "position", out.cameraPosition);
-        getVec3(*c, "look_at", out.cameraLookAt);
-        getFloat(*c, "fovy", out.cameraFovyDegrees);
+    if (const Value c = getObject(root, "camera"); c.valid()) {
+        getVec3(c, "position", out.cameraPosition);
+        getVec3(c, "look_at", out.cameraLookAt);
+        getFloat(c, "fovy", out.cameraFovyDegrees);
     }
     return true;
 }

@@ -114,6 +114,33 @@ def test_json_quirks(tmp_path, capfd):
     assert bytes(cam) == bytes(ref)
 
 
+def test_json_reader_edge_cases(tmp_path):
+    # nlohmann semantics the loader can observe: duplicate keys (last wins), escapes, BOM, an
+    # integer token beyond int64 (a float value of an *integer* token), exponent floats, nesting
+    text = ('\ufeff{"objects": [{"type": "CUBE", "type": "S\\u0050HERE", "position": [1e0, 18446744073709551557, 99999999999999999999],'
+            ' "material": {"roughness": 0.25, "roughness": 7.5e-1, "extra": [[[{}]]], "baseColor": [0.5, 1, 2.0]}}],'
+            ' "camera": {"fovy": 4.5e1}}')
+    p = tmp_path / "e.json"
+    p.write_bytes(text.encode("utf-8"))
+    s = pa.Scene(p, 10, 10)
+    objs, _ = s.objects()
+    o = objs[0]
+    assert o.type == 0                                   # "S\u0050HERE" -> "SPHERE", the last "type" wins
+    assert abs(o.roughness - 0.75) < 1e-7                # the last "roughness" wins
+    assert list(o.base_color) == [0.5, 1.0, 2.0]          # int components accepted by get<float>()
+    cam = s.camera()
+    ref = pa.make_camera((0, 0, 0), (0, 0, -1), fovy_radians=pa.radians(45.0), aspect=1.0)
+    assert bytes(cam) == bytes(ref)
+    # the same object written plainly gives the same record: y is a uint64 token converted to float
+    # directly (not via double), z = float(1e20)
+    y = float(np.float32(18446744073709551557))
+    plain = tmp_path / "plain.json"
+    plain.write_text(json.dumps({"objects": [{"type": "SPHERE", "position": [1.0, y, 1e20],
+                                              "material": {"roughness": 0.75, "baseColor": [0.5, 1.0, 2.0]}}]}))
+    objs2, _ = pa.Scene(plain, 10, 10).objects()
+    assert bytes(objs) == bytes(objs2)
+
+
 def test_scene_errors(tmp_path):
     with pytest.raises(pa.PathtracerError, match="Failed to open"):
         pa.Scene(tmp_path / "missing.json", 8, 8)
@@ -195,3 +222,22 @@ def test_camera_matches_oracle():
         o = po.Camera()
         L.or_camera_make(po.f3(pos), po.f3(look), po.f3([0, 1, 0]), L.or_radians(fovy), float(np.float32(aspect)), C.byref(o))
         assert bytes(c) == bytes(o)
+
+
+def test_parallel_bvh_build_identical_to_sequential(tmp_path, root, monkeypatch):
+    # the multi-threaded build (independent subtrees, rebased concatenation) must give the
+    # sequential layout node for node and the same element order
+    import subprocess
+    import sys
+    path = tmp_path / "grid.json"
+    subprocess.run([sys.executable, str(root / "tools" / "make_stress_scene.py"), str(path), "--grid", "110"],
+                   check=True, capture_output=True)
+    monkeypatch.setenv("PT_BVH_THREADS", "1")
+    seq = pa.Scene(path, 64, 64)
+    n1, p1 = seq.bvh()
+    monkeypatch.setenv("PT_BVH_THREADS", "8")
+    par = pa.Scene(path, 64, 64)
+    n8, p8 = par.bvh()
+    assert seq.object_count == par.object_count > 10000
+    assert bytes(n1) == bytes(n8) and bytes(p1) == bytes(p8)
+    assert par.timing()["bvh_ms"] > 0.0
