@@ -8,7 +8,11 @@ sky texture, RNG state, accumulation buffer).
 
 N GPUs (torchrun, one process per GPU, RCCL): the image rows are interleaved over the ranks
 (row r -> rank r mod N), each rank renders its rows, and the HDR framebuffer is gathered to rank 0
-over RCCL inside the timed region (strong scaling: the same 1080p x 1024 spp image for every N).
+over RCCL inside the timed region.  Default weak scaling: each GPU keeps one 1080p frame's worth of
+pixels (the image grows by sqrt(N) per axis: 2720x1528, 3840x2160 (= C4), 5432x3056 at 1024 spp);
+`--scaling strong` renders the same 1080p image for every N.  A pixel's samples are one serial
+XORWOW stream, so strong scaling of a 1080p frame is bounded by its most expensive 8x8 tile
+(DESIGN.md "Multi-GPU"; tools/scale_sim.py).
 
 Printed JSON line (rank 0): value = samples of the whole image / step time; roofline = the trace
 kernel's algorithmic bytes (counted node/prim/material/sky reads + per-pixel
@@ -19,6 +23,7 @@ from __future__ import annotations
 
 import argparse
 import json
+import math
 import os
 import pathlib
 import sys
@@ -43,6 +48,8 @@ def parse_args():
     p.add_argument("--spp", type=int, default=1024)
     p.add_argument("--chunk", type=int, default=8)
     p.add_argument("--cpu-baseline", type=int, default=1, help="time the oracle on a bounded sample (rank 0, N=1)")
+    p.add_argument("--scaling", choices=["weak", "strong"], default="weak",
+                   help="weak: per-GPU work fixed (image grows with N); strong: the same 1080p image for every N")
     p.add_argument("--cpu-threads", type=int, default=0)
     p.add_argument("--cpu-spp", type=int, default=192)
     return p.parse_args()
@@ -96,6 +103,11 @@ def main():
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
     n = max(1, world if world > 1 else args.gpus)
     W, H, spp, chunk = args.width, args.height, args.spp, args.chunk
+    if args.scaling == "weak" and n > 1:
+        # weak scaling: every GPU keeps one 1080p frame's worth of pixels; the image grows by
+        # sqrt(N) per axis (N = 4 is 3840x2160, the C4 resolution), rows interleaved over ranks
+        W = int(round(W * math.sqrt(n) / 8.0)) * 8
+        H = int(round(H * math.sqrt(n) / 8.0)) * 8
     chunks = spp // chunk
     assert chunks * chunk == spp, "spp must be a multiple of --chunk"
 
@@ -179,12 +191,13 @@ def main():
         "warmup": args.warmup,
         "ms_per_step": round(ms_per_step, 3),
         "higher_is_better": True,
-        "scaling": "strong",
+        "scaling": args.scaling,
         "vs_baseline": None,
         "dtype": "f32",
         "data": "synthetic sky (scenes/skybox.hdr), reference scene generated_scene.json",
         "config": {"workload": workload, "scene": "generated_scene.json (484 quadrics)", "width": W, "height": H,
-                   "spp": spp, "render_calls_per_step": chunks, "parallelism": f"rows interleaved x{n}, RCCL gather"},
+                   "spp": spp, "render_calls_per_step": chunks, "parallelism": f"rows interleaved x{n}, RCCL gather",
+                   "per_gpu_pixels": (W * H + n - 1) // n},
         "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                      "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic,
                      "kernel": "trace_kernel", "avg_launch_ms": round(avg_launch_s * 1e3, 3),

@@ -62,6 +62,7 @@ struct TraceParams {
     uint32_t cnodeCount, rootWord;
     float rootBox[6];           // (min.x, max.x, min.y, max.y, min.z, max.z) of the root
     const uint32_t* order;      // tile dispatch order (null: row-major), see "Tile scheduling"
+    uint32_t scatterWaves;      // != 0: scattered pixel mapping over this many waves (pixel_of)
     uint32_t* tileCost;         // per-tile shader-clock cycles of this launch (null: not recorded)
     DevCamera cam;
 };
@@ -1050,12 +1051,23 @@ struct PixelCtx {
 PT_DEV PixelCtx pixel_of(const TraceParams& P, uint32_t tile, uint32_t lane)
 {
     PixelCtx pc;
+    pc.npix = (size_t)P.rows * P.width;
+    if (P.scatterWaves) {
+        // scattered mapping: lane k of wave w takes local pixel k * waves + w, so every wave holds
+        // pixels from the whole tile of rows and all waves cost about the same
+        const size_t li = (size_t)lane * P.scatterWaves + tile;
+        pc.valid = tile < P.scatterWaves && li < pc.npix;
+        pc.li = pc.valid ? li : 0;
+        const uint32_t ly = (uint32_t)(pc.li / P.width);
+        pc.px = (uint32_t)(pc.li - (size_t)ly * P.width);
+        pc.py = P.rowOffset + ly * P.rowStride;
+        return pc;
+    }
     const uint32_t tileX = tile % P.tilesX, tileY = tile / P.tilesX;
     pc.px = tileX * 8u + (lane & 7u);
     const uint32_t ly = tileY * 8u + (lane >> 3);
     pc.valid = tileY < P.tilesY && pc.px < P.width && ly < P.rows;
     pc.py = P.rowOffset + ly * P.rowStride;
-    pc.npix = (size_t)P.rows * P.width;
     pc.li = (size_t)ly * P.width + pc.px;
     return pc;
 }
@@ -1772,6 +1784,7 @@ static int render_impl(pt_context* ctx, const pt_camera* cam, uint32_t spp, uint
     const bool sorted = ctx->schedule == 0;
     P.order = (sorted && ctx->orderValid) ? ctx->order : nullptr;
     P.tileCost = sorted ? ctx->tileCost : nullptr;
+    P.scatterWaves = ctx->schedule == 2 ? (uint32_t)(((size_t)ctx->rows * ctx->width + 63) / 64) : 0u;
     if (stats) PT_HIP_CHECK(ctx, hipMemsetAsync(ctx->stats, 0, 16 * sizeof(unsigned long long), ctx->stream));
     PT_HIP_CHECK(ctx, hipEventRecord(ctx->ev0, ctx->stream));
     const int variant = pick_variant(ctx);
@@ -1815,7 +1828,7 @@ static int render_impl(pt_context* ctx, const pt_camera* cam, uint32_t spp, uint
 
 PT_API int pt_set_schedule(pt_context* ctx, int mode)
 {
-    if (!ctx || mode < 0 || mode > 1) return PT_ERR_ARG;
+    if (!ctx || mode < 0 || mode > 2) return PT_ERR_ARG;
     ctx->schedule = mode;
     ctx->orderStale = true;
     return PT_OK;

