@@ -85,8 +85,10 @@ PT_DEV f3 tex2d(const DevTex& t, float u, float v)
     int32_t i0 = (fx > -1.0e9f && fx < 1.0e9f) ? (int32_t)fx : 0;
     int32_t j0 = (fy > -1.0e9f && fy < 1.0e9f) ? (int32_t)fy : (fy > 0.0f ? h : -1);
     int32_t i1 = i0 + 1, j1 = j0 + 1;
-    i0 = ((i0 % w) + w) % w;
-    i1 = ((i1 % w) + w) % w;
+    // wrap: u - floor(u) lies in [0, 1] (or is NaN, giving i0 = 0), so fx lies in [-1, w - 1] and
+    // i0 in [-1, w - 1], i1 in [0, w]: one conditional add/subtract equals ((i % w) + w) % w here
+    i0 = i0 < 0 ? i0 + w : i0;
+    i1 = i1 >= w ? i1 - w : i1;
     j0 = j0 < 0 ? 0 : (j0 > h - 1 ? h - 1 : j0);
     j1 = j1 < 0 ? 0 : (j1 > h - 1 ? h - 1 : j1);
     const float4 T00 = t.texels[(size_t)j0 * t.width + (size_t)i0];
@@ -767,15 +769,15 @@ PT_DEV Surface surface_of(const float4& r0, const float4& r1, const float4& r2, 
         if (needUV) {
             const float theta = acos_(n.y);
             const float phi = atan2_(n.z, n.x);
-            u = 1.0f - phi / kTwoPi;
-            v = theta / kPi;
+            u = 1.0f - div_two_pi(phi);
+            v = div_pi(theta);
         }
         break;
     case CYLINDER:
         n = mk(lp.x, 0.0f, lp.z);
         if (needUV) {
             const float phi = atan2_(n.z, n.x);
-            u = 1.0f - phi / kTwoPi;
+            u = 1.0f - div_two_pi(phi);
             v = 1.0f - (lp.y * 0.5f + 0.5f);
         }
         break;
@@ -899,8 +901,8 @@ PT_DEV bool shade(const TraceParams& P, const float4* __restrict__ prims, uint32
             if (STATS) { cnt.sky++; wave_tick(cnt.w_sky); }
             const float theta = acos_(ps.d.y);
             const float phi = atan2_(ps.d.z, ps.d.x);
-            const float v = theta / kPi;
-            const float u = phi / kTwoPi;
+            const float v = div_pi(theta);
+            const float u = div_two_pi(phi);
             sky = tex2d(P.textures[P.skybox - 1], u, v);
         }
         ps.L = add(ps.L, mul(ps.T, sky));
@@ -958,7 +960,7 @@ PT_DEV bool shade(const TraceParams& P, const float4* __restrict__ prims, uint32
     const float sq = sqrt_rn(specular ? rnd0 : rnd1);
     if (mtype == 0u) {                                                        // LAMBERT (Material.inl:67-72)
         dir = mk(cs * sqrt_rn(1.0f - rnd1), sn * sqrt_rn(1.0f - rnd1), sq);       // cosine_sample
-        pdf = dir.z / kPi;
+        pdf = div_pi(dir.z);
         att = scale(kInvPi, base);
     } else if (mtype <= 2u) {
         if (specular) {
@@ -982,7 +984,7 @@ PT_DEV bool shade(const TraceParams& P, const float4* __restrict__ prims, uint32
                 pdf = ggxPdf;
                 att = kS;
             } else {
-                const float cosinePdf = dir.z / kPi;
+                const float cosinePdf = div_pi(dir.z);
                 pdf = (ggxPdf + cosinePdf) * 0.5f;
                 att = add(scale(1.0f - metal, scale(kInvPi, base)), kS);
             }

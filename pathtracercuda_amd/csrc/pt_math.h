@@ -54,6 +54,26 @@ PT_DEV float sqrt_rn(float x)
     return sqrtf(x);
 }
 
+// x / c for the constants c = PI, 2 PI: q = x * RN(1/c) corrected once with the exact residual
+// fma(-c, q, x) (Markstein), behind the guard 2^-100 <= |x| <= 2^100 (other inputs, incl. 0,
+// inf and NaN, divide).  Checked against the correctly rounded quotient for all 2^32 inputs by
+// tools/fp_exhaustive.hip.
+template <int K>
+PT_DEV float div_const(float x)
+{
+    constexpr float c = K == 1 ? 3.14159265358979323846f : 2.0f * 3.14159265358979323846f;
+    constexpr float y = 1.0f / c;                    // RN(1/c), folded at compile time
+    const float ax = __builtin_fabsf(x);
+    if (ax >= 0x1p-100f && ax <= 0x1p100f) {
+        const float q = x * y;
+        const float r = __builtin_fmaf(-c, q, x);
+        return __builtin_fmaf(r, y, q);
+    }
+    return x / c;
+}
+PT_DEV float div_pi(float x) { return div_const<1>(x); }
+PT_DEV float div_two_pi(float x) { return div_const<2>(x); }
+
 struct f3 { float x, y, z; };
 
 PT_DEV f3 mk(float x, float y, float z) { return f3{x, y, z}; }

@@ -10,7 +10,7 @@
 
 #include "../pathtracercuda_amd/csrc/pt_math.h"
 
-#define NSEQ 6
+#define NSEQ 8
 __device__ unsigned long long g_bad[NSEQ];
 __device__ uint32_t g_first[NSEQ][8];
 
@@ -46,6 +46,9 @@ __global__ void check(uint32_t base)
     const float rm = __builtin_fmaf(-sm, s, x), rp = __builtin_fmaf(-sp, s, x);
     const float sc = rp > 0.0f ? sp : (rm <= 0.0f ? sm : s);
     check_one(5, same(sc, ref_sqrt), xb);
+    // x / pi and x / (2 pi) (the sky's theta / PI, phi / (2 PI), the cosine pdf z / PI)
+    check_one(6, same(pt::div_pi(x), x / pt::kPi), xb);
+    check_one(7, same(pt::div_two_pi(x), x / pt::kTwoPi), xb);
 }
 
 int main()
@@ -61,7 +64,7 @@ int main()
     if (hipMemcpyFromSymbol(bad, HIP_SYMBOL(g_bad), sizeof(bad)) != hipSuccess) return 2;
     if (hipMemcpyFromSymbol(first, HIP_SYMBOL(g_first), sizeof(first)) != hipSuccess) return 2;
     const char* names[NSEQ] = {"rcp_rn", "sqrt_rn", "diag_rcp_raw_all_inputs", "diag_rcp_newton_unguarded",
-                               "diag_sqrt_raw_all_inputs", "diag_sqrt_corrected_unguarded"};
+                               "diag_sqrt_raw_all_inputs", "diag_sqrt_corrected_unguarded", "div_pi", "div_two_pi"};
     printf("{\n  \"inputs\": 4294967296,\n");
     for (int k = 0; k < NSEQ; ++k) {
         printf("  \"%s\": {\"mismatches\": %llu, \"first\": [", names[k], bad[k]);
