@@ -875,7 +875,7 @@ struct PathState {
     f3 o, d;          // current ray
     f3 L, T;          // radiance and throughput of the current path (trace.cu:104-105)
     f3 color;         // sum of the finished paths of the current render() call (trace.cu:186)
-    f3 accum;         // accumulation buffer value of this pixel
+    uint32_t li;      // local pixel index: the accumulation value lives in P.accum[li]
     uint32_t s, c, bounce;
     bool alive;
 };
@@ -1009,8 +1009,15 @@ PT_DEV void finish_path(const TraceParams& P, PathState& ps, Xorwow& rng, float 
     ps.color = add(ps.color, ps.L);
     if (STATS) cnt.samples++;
     if (++ps.s == P.spp) {
+        // fold the call into the accumulation value (trace.cu:196-198); the value is read and
+        // written in global memory once per call rather than held in registers for the launch
         const bool ignore = (ps.c == 0) && P.ignoreFirst;
-        ps.accum = ignore ? ps.color : add(ps.color, ps.accum);
+        f3 acc = ps.color;
+        if (!ignore) {
+            const float4 old = P.accum[ps.li];
+            acc = add(ps.color, mk(old.x, old.y, old.z));
+        }
+        P.accum[ps.li] = make_float4(acc.x, acc.y, acc.z, 1.0f);
         ps.color = splat(0.0f);
         ps.s = 0;
         if (++ps.c == P.chunks) ps.alive = false;
@@ -1082,8 +1089,7 @@ PT_DEV void load_pixel(const TraceParams& P, const PixelCtx& pc, Xorwow& rng, Pa
     rng.v2 = P.rng[3 * pc.npix + pc.li];
     rng.v3 = P.rng[4 * pc.npix + pc.li];
     rng.v4 = P.rng[5 * pc.npix + pc.li];
-    const float4 acc = P.accum[pc.li];
-    ps.accum = mk(acc.x, acc.y, acc.z);
+    ps.li = (uint32_t)pc.li;
     ps.color = splat(0.0f);
     ps.L = splat(0.0f);
     ps.T = splat(1.0f);
@@ -1093,7 +1099,6 @@ PT_DEV void load_pixel(const TraceParams& P, const PixelCtx& pc, Xorwow& rng, Pa
 
 PT_DEV void store_pixel(const TraceParams& P, const PixelCtx& pc, const Xorwow& rng, const PathState& ps)
 {
-    P.accum[pc.li] = make_float4(ps.accum.x, ps.accum.y, ps.accum.z, 1.0f);
     P.rng[pc.li] = rng.d;
     P.rng[pc.npix + pc.li] = rng.v0;
     P.rng[2 * pc.npix + pc.li] = rng.v1;
