@@ -1398,7 +1398,11 @@ static hipError_t launch_one(const TraceParams& P, hipStream_t stream)
     const size_t sceneBytes = ((SL >= 1 ? nodeF4 : 0) + (SL >= 2 ? 4 * (size_t)P.primCount : 0)) * sizeof(float4);
     const size_t lds = sceneBytes + (size_t)WPB * P.stackDepth * 64 * (WW >= 3 ? 8 : 4);
     if (WW >= 3 && P.cnodes == nullptr) return launch_one<STATS, SL, WPB, 1, MINW>(P, stream);  // no child-box layout
-    if (lds > 160 * 1024) return hipErrorInvalidValue;
+    if (lds > 160 * 1024) {
+        // scene too large to stage in LDS: the same variant reading the scene through the caches
+        if (SL > 0) return launch_one<STATS, 0, WPB, WW, MINW>(P, stream);
+        return hipErrorInvalidValue;                   // the stacks alone exceed the LDS
+    }
     static bool attrSet = false;
     if (!attrSet) {
         hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(&trace_kernel<STATS, SL, WPB, WW, MINW>),
