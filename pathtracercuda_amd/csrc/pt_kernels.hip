@@ -1471,11 +1471,11 @@ static int pick_variant(const pt_context* ctx)
     // wins on every scene; the child-box records are staged in LDS when they fit in 48 KB
     // (cornell, the 484-object scene) and read through the caches otherwise (100k objects).
     // Scenes outside the child-box encoding fall back to the node-at-a-time walk (launch_one).
-    // With the records in LDS the resumable form (variant 28: the wave shades its finished lanes
-    // once at most 12/64 still walk) wins; deep BVHs read through the caches gain most from
-    // speculative traversal (variant 22).
+    // The resumable form wins everywhere (the wave shades its finished lanes once at most 12/64
+    // (LDS records, variant 28) or 8/64 (records read through the caches, variant 26, the
+    // 100k-object scene) still walk).
     const size_t cbBytes = 4 * (size_t)ctx->cnodeCount * sizeof(float4);
-    if (ctx->cnodes) return cbBytes <= 48 * 1024 ? 28 : 22;
+    if (ctx->cnodes) return cbBytes <= 48 * 1024 ? 28 : 26;
     const size_t nodeBytes = 2 * (size_t)ctx->nodeCount * sizeof(float4);
     return nodeBytes <= 48 * 1024 ? 6 : 4;
 }
