@@ -101,7 +101,10 @@ def main():
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
-    n = max(1, world if world > 1 else args.gpus)
+    if world == 1 and args.gpus > 1:
+        print(f"bench.py: --gpus {args.gpus} needs one process per GPU (torch.distributed.run "
+              f"--nproc-per-node {args.gpus}); running on 1 GPU", file=sys.stderr)
+    n = max(1, world)
     W, H, spp, chunk = args.width, args.height, args.spp, args.chunk
     if args.scaling == "weak" and n > 1:
         # weak scaling: every GPU keeps one 1080p frame's worth of pixels; the image grows by
