@@ -27,6 +27,7 @@
 #include <string>
 #include <vector>
 #include <algorithm>
+#include <atomic>
 
 #include "pt_math.h"
 #include "../../include/pt_hip.h"
@@ -1403,12 +1404,17 @@ static hipError_t launch_one(const TraceParams& P, hipStream_t stream)
         if (SL > 0) return launch_one<STATS, 0, WPB, WW, MINW>(P, stream);
         return hipErrorInvalidValue;                   // the stacks alone exceed the LDS
     }
-    static bool attrSet = false;
-    if (!attrSet) {
+    // the dynamic-LDS limit is raised once per device (contexts on several devices may run on
+    // several host threads, as the CLI's -gpus mode does)
+    static std::atomic<uint64_t> attrSet{0};
+    int dev = 0;
+    (void)hipGetDevice(&dev);
+    const uint64_t bit = 1ull << (dev & 63);
+    if (!(attrSet.load() & bit)) {
         hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(&trace_kernel<STATS, SL, WPB, WW, MINW>),
                                            hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
         if (e != hipSuccess) return e;
-        attrSet = true;
+        attrSet.fetch_or(bit);
     }
     const uint32_t tiles = P.tilesX * P.tilesY;
     const unsigned blocks = (tiles + WPB - 1) / WPB;
