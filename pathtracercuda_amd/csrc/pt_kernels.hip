@@ -64,6 +64,8 @@ struct TraceParams {
     float rootBox[6];           // (min.x, max.x, min.y, max.y, min.z, max.z) of the root
     const uint32_t* order;      // tile dispatch order (null: row-major), see "Tile scheduling"
     uint32_t scatterWaves;      // != 0: scattered pixel mapping over this many waves (pixel_of)
+    uint32_t* tileCursor;       // persistent variants: {next dispatch slot, waves finished}, rewound by the last wave
+    uint32_t numSlots;          // dispatch slots = 8x8 tiles
     uint32_t* tileCost;         // per-tile shader-clock cycles of this launch (null: not recorded)
     DevCamera cam;
 };
@@ -1052,6 +1054,16 @@ PT_DEV void flush_counters(const TraceParams& P, const Counters& cnt)
     atomicAdd(&P.stats[14], (unsigned long long)cnt.cyc_total);
 }
 
+// One atomic per wave: the first active lane adds n to *cursor and broadcasts the old value.
+PT_DEV uint32_t wave_fetch(uint32_t* cursor, uint32_t n)
+{
+    const unsigned long long m = __ballot(1);
+    const uint32_t leader = (uint32_t)(__ffsll((long long)m) - 1);
+    uint32_t base = 0;
+    if ((threadIdx.x & 63u) == leader) base = atomicAdd(cursor, n);
+    return (uint32_t)__shfl((int)base, (int)leader, 64);
+}
+
 struct PixelCtx {
     bool valid;
     uint32_t px, py;
@@ -1114,7 +1126,10 @@ PT_DEV void store_pixel(const TraceParams& P, const PixelCtx& pc, const Xorwow& 
 // SCENE_LDS, then WPB wave stacks of stackDepth x 64 u32.
 // ---------------------------------------------------------------------------------------------
 // SL = 0: scene read through the caches; 1: BVH nodes staged in LDS; 2: nodes and primitives in LDS.
-template <bool STATS, int SL, int WPB, int WW, int MINW>
+// One wave = one 8x8 tile.  PERSIST: the grid holds only the resident waves, and each wave takes
+// the next dispatch slot from a global counter when its tile is done, so a wave never waits for
+// the other waves of its workgroup (which would keep the group's LDS and slots idle).
+template <bool STATS, int SL, int WPB, int WW, int MINW, bool PERSIST = false>
 __global__ void __launch_bounds__(WPB * 64, MINW) trace_kernel(TraceParams P)
 {
     extern __shared__ float4 lds4[];
@@ -1134,11 +1149,13 @@ __global__ void __launch_bounds__(WPB * 64, MINW) trace_kernel(TraceParams P)
     // wave stacks: stackDepth x 64 entries of u32 (node index), or of uint2 (word, lo) for WW == 3
     uint32_t* stack = reinterpret_cast<uint32_t*>(lds4 + sceneF4) + (WW >= 3 ? 2u : 1u) * wave * P.stackDepth * 64u +
                       (WW >= 3 ? 2u : 1u) * lane;
-    const uint32_t slot = blockIdx.x * (uint32_t)WPB + wave;
+    Counters cnt = {};
+    uint32_t slot = PERSIST ? wave_fetch(P.tileCursor, 1u) : blockIdx.x * (uint32_t)WPB + wave;
+    for (;;) {
+    if (PERSIST && slot >= P.numSlots) break;
     const uint32_t tile = P.order ? P.order[slot] : slot;
     const PixelCtx pc = pixel_of(P, tile, lane);
     const uint64_t tWave = __builtin_amdgcn_s_memtime();
-    Counters cnt = {};
     if (pc.valid) {
         Xorwow rng;
         PathState ps;
@@ -1175,6 +1192,17 @@ __global__ void __launch_bounds__(WPB * 64, MINW) trace_kernel(TraceParams P)
     }
     if (P.tileCost && lane == 0 && tile < P.tilesX * P.tilesY)
         P.tileCost[tile] = (uint32_t)min(__builtin_amdgcn_s_memtime() - tWave, (uint64_t)0xffffffffu);
+    if (!PERSIST) break;
+    slot = wave_fetch(P.tileCursor, 1u);
+    }
+    if (PERSIST) {
+        // the last wave to leave rewinds the cursor for the next launch (every wave has made its
+        // final fetch before it counts itself out), so no memset precedes the launch
+        if (wave_fetch(P.tileCursor + 1, 1u) == gridDim.x * (uint32_t)WPB - 1 && lane == 0) {
+            P.tileCursor[0] = 0;
+            P.tileCursor[1] = 0;
+        }
+    }
     flush_counters<STATS>(P, cnt);
 }
 
@@ -1349,6 +1377,7 @@ struct pt_context {
     // tile scheduling: per-tile cost of the last launch and the cost-sorted dispatch order
     uint32_t* tileCost = nullptr;
     uint32_t* order = nullptr;
+    uint32_t* tileCursor = nullptr;   // persistent variants
     uint32_t* sortKeys = nullptr; // radix-sort scratch: sorted costs, tile ids, temp storage
     uint32_t* tileIds = nullptr;
     void* sortTemp = nullptr;
@@ -1392,16 +1421,16 @@ static int fail(pt_context* ctx, int code, const char* msg)
 }
 
 // Kernel variants (workgroup size, scene staged in LDS or read through the caches).
-template <bool STATS, int SL, int WPB, int WW, int MINW>
+template <bool STATS, int SL, int WPB, int WW, int MINW, bool PERSIST = false>
 static hipError_t launch_one(const TraceParams& P, hipStream_t stream)
 {
     const size_t nodeF4 = WW >= 3 ? 4 * (size_t)P.cnodeCount : 2 * (size_t)P.nodeCount;
     const size_t sceneBytes = ((SL >= 1 ? nodeF4 : 0) + (SL >= 2 ? 4 * (size_t)P.primCount : 0)) * sizeof(float4);
     const size_t lds = sceneBytes + (size_t)WPB * P.stackDepth * 64 * (WW >= 3 ? 8 : 4);
-    if (WW >= 3 && P.cnodes == nullptr) return launch_one<STATS, SL, WPB, 1, MINW>(P, stream);  // no child-box layout
+    if (WW >= 3 && P.cnodes == nullptr) return launch_one<STATS, SL, WPB, 1, MINW, PERSIST>(P, stream);  // no child-box layout
     if (lds > 160 * 1024) {
         // scene too large to stage in LDS: the same variant reading the scene through the caches
-        if (SL > 0) return launch_one<STATS, 0, WPB, WW, MINW>(P, stream);
+        if (SL > 0) return launch_one<STATS, 0, WPB, WW, MINW, PERSIST>(P, stream);
         return hipErrorInvalidValue;                   // the stacks alone exceed the LDS
     }
     // the dynamic-LDS limit is raised once per device (contexts on several devices may run on
@@ -1411,14 +1440,32 @@ static hipError_t launch_one(const TraceParams& P, hipStream_t stream)
     (void)hipGetDevice(&dev);
     const uint64_t bit = 1ull << (dev & 63);
     if (!(attrSet.load() & bit)) {
-        hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(&trace_kernel<STATS, SL, WPB, WW, MINW>),
+        hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(&trace_kernel<STATS, SL, WPB, WW, MINW, PERSIST>),
                                            hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
         if (e != hipSuccess) return e;
         attrSet.fetch_or(bit);
     }
     const uint32_t tiles = P.tilesX * P.tilesY;
-    const unsigned blocks = (tiles + WPB - 1) / WPB;
-    trace_kernel<STATS, SL, WPB, WW, MINW><<<blocks, WPB * 64, lds, stream>>>(P);
+    unsigned blocks = (tiles + WPB - 1) / WPB;
+    if (PERSIST) {
+        // resident workgroups per device, cached per instantiation; a grid that fits in one
+        // pass gains nothing from the cursor and runs the plain kernel
+        static std::atomic<int> resident[64];
+        int cap = resident[dev & 63].load();
+        if (cap == 0) {
+            int cus = 0, perCu = 0;
+            hipError_t e = hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
+            if (e == hipSuccess)
+                e = hipOccupancyMaxActiveBlocksPerMultiprocessor(
+                    &perCu, reinterpret_cast<const void*>(&trace_kernel<STATS, SL, WPB, WW, MINW, PERSIST>), WPB * 64, lds);
+            if (e != hipSuccess) return e;
+            cap = std::max(cus, 1) * std::max(perCu, 1);
+            resident[dev & 63].store(cap);
+        }
+        if (blocks <= (unsigned)cap) return launch_one<STATS, SL, WPB, WW, MINW, false>(P, stream);
+        blocks = (unsigned)cap;
+    }
+    trace_kernel<STATS, SL, WPB, WW, MINW, PERSIST><<<blocks, WPB * 64, lds, stream>>>(P);
     return hipGetLastError();
 }
 
@@ -1465,6 +1512,16 @@ static hipError_t launch_variant(int v, const TraceParams& P, hipStream_t stream
     case 27: return launch_one<STATS, 1, 4, 102, 5>(P, stream);  // <= 2/64
     case 28: return launch_one<STATS, 1, 4, 112, 5>(P, stream);  // <= 12/64
     case 29: return launch_one<STATS, 1, 4, 108, 6>(P, stream);
+    case 30: return launch_one<STATS, 1, 4, 112, 5, true>(P, stream);     // persistent waves
+    case 31: return launch_one<STATS, 0, 4, 108, 5, true>(P, stream);
+    case 32: return launch_one<STATS, 1, 8, 112, 5, true>(P, stream);
+    case 33: return launch_one<STATS, 1, 2, 112, 5, true>(P, stream);
+    case 34: return launch_one<STATS, 0, 4, 112, 5, true>(P, stream);
+    case 35: return launch_one<STATS, 1, 4, 104, 5, true>(P, stream);
+    case 36: return launch_one<STATS, 1, 4, 112, 6, true>(P, stream);
+    case 37: return launch_one<STATS, 1, 4, 120, 5, true>(P, stream);
+    case 38: return launch_one<STATS, 1, 4, 116, 5, true>(P, stream);
+    case 39: return launch_one<STATS, 0, 4, 116, 5, true>(P, stream);
     default: return launch_one<STATS, 0, 4, 1, 1>(P, stream);
     }
 }
@@ -1477,11 +1534,11 @@ static int pick_variant(const pt_context* ctx)
     // wins on every scene; the child-box records are staged in LDS when they fit in 48 KB
     // (cornell, the 484-object scene) and read through the caches otherwise (100k objects).
     // Scenes outside the child-box encoding fall back to the node-at-a-time walk (launch_one).
-    // The resumable form wins everywhere (the wave shades its finished lanes once at most 12/64
-    // (LDS records, variant 28) or 8/64 (records read through the caches, variant 26, the
-    // 100k-object scene) still walk).
+    // The resumable form wins everywhere (the wave shades its finished lanes once at most 16/64
+    // still walk), and so do persistent waves pulling tiles from a cursor (variants 30/34: +6% on
+    // the 484-object scene, +11% on 100k objects over the one-tile-per-wave grid, variants 28/26).
     const size_t cbBytes = 4 * (size_t)ctx->cnodeCount * sizeof(float4);
-    if (ctx->cnodes) return cbBytes <= 48 * 1024 ? 28 : 26;
+    if (ctx->cnodes) return cbBytes <= 48 * 1024 ? 30 : 34;
     const size_t nodeBytes = 2 * (size_t)ctx->nodeCount * sizeof(float4);
     return nodeBytes <= 48 * 1024 ? 6 : 4;
 }
@@ -1548,6 +1605,7 @@ PT_API void pt_destroy(pt_context* ctx)
     (void)hipFree(ctx->cnodes);
     (void)hipFree(ctx->tileCost);
     (void)hipFree(ctx->order);
+    (void)hipFree(ctx->tileCursor);
     (void)hipFree(ctx->ldr);
     (void)hipFree(ctx->sortKeys);
     (void)hipFree(ctx->tileIds);
@@ -1802,6 +1860,12 @@ static int render_impl(pt_context* ctx, const pt_camera* cam, uint32_t spp, uint
     P.order = (sorted && ctx->orderValid) ? ctx->order : nullptr;
     P.tileCost = sorted ? ctx->tileCost : nullptr;
     P.scatterWaves = ctx->schedule == 2 ? (uint32_t)(((size_t)ctx->rows * ctx->width + 63) / 64) : 0u;
+    if (!ctx->tileCursor) {
+        PT_HIP_CHECK(ctx, hipMalloc(&ctx->tileCursor, 2 * sizeof(uint32_t)));
+        PT_HIP_CHECK(ctx, hipMemset(ctx->tileCursor, 0, 2 * sizeof(uint32_t)));
+    }
+    P.tileCursor = ctx->tileCursor;
+    P.numSlots = tiles;
     if (stats) PT_HIP_CHECK(ctx, hipMemsetAsync(ctx->stats, 0, 16 * sizeof(unsigned long long), ctx->stream));
     PT_HIP_CHECK(ctx, hipEventRecord(ctx->ev0, ctx->stream));
     const int variant = pick_variant(ctx);
@@ -1942,7 +2006,7 @@ PT_API uint32_t pt_local_rows(const pt_context* ctx) { return ctx ? ctx->rows : 
 
 PT_API int pt_set_kernel_variant(pt_context* ctx, int variant)
 {
-    if (!ctx || variant < 0 || variant > 29) return PT_ERR_ARG;
+    if (!ctx || variant < 0 || variant > 39) return PT_ERR_ARG;
     ctx->variant = variant;
     return PT_OK;
 }

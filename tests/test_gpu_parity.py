@@ -67,7 +67,7 @@ def test_render_bitexact(gpu_available, scenes, name, W, H, spp, chunks):
     assert pt.frames == ref.frames == chunks
 
 
-@pytest.mark.parametrize("variant", range(1, 30))
+@pytest.mark.parametrize("variant", range(1, 40))
 def test_every_kernel_variant_bitexact(gpu_available, scenes, variant):
     # all trace-kernel variants (schedules, LDS staging, occupancy) produce the reference's bits
     pt, cam, ref, osc = pair(scenes / "test_shapes.scene.json", 72, 40)
@@ -76,6 +76,23 @@ def test_every_kernel_variant_bitexact(gpu_available, scenes, variant):
     ref.render(osc.camera, 4, True, chunks=2)
     assert_bitexact(pt.accum(), ref.accum, f"variant {variant}")
     assert np.array_equal(pt.rng_state(), ref.rng_array())
+
+
+def test_persistent_variants_large_grid(gpu_available, scenes):
+    # the persistent variants fall back to the plain kernel when the grid fits on the chip in one
+    # pass, so run them on a frame with more tiles than resident waves, several launches in a row
+    # (the last wave of each launch rewinds the tile cursor for the next), against variant 1
+    pt = pa.Pathtracer(1280, 720)
+    cam = pt.load_scene(scenes / "generated_scene.scene.json")
+    st = pt.rng_state()
+    pt.set_kernel_variant(1)
+    pt.render(cam, 3, True, chunks=3)
+    want = pt.accum().view(np.uint32).copy()       # bits: the reference's NaN pixels stay NaN
+    for variant in range(30, 40):
+        pt.set_kernel_variant(variant)
+        pt.set_rng_state(st)
+        pt.render(cam, 3, True, chunks=3)
+        assert np.array_equal(pt.accum().view(np.uint32), want), f"variant {variant}"
 
 
 @pytest.mark.parametrize("nprims", [484, 200])
