@@ -1534,7 +1534,7 @@ static int pick_variant(const pt_context* ctx)
     // wins on every scene; the child-box records are staged in LDS when they fit in 48 KB
     // (cornell, the 484-object scene) and read through the caches otherwise (100k objects).
     // Scenes outside the child-box encoding fall back to the node-at-a-time walk (launch_one).
-    // The resumable form wins everywhere (the wave shades its finished lanes once at most 16/64
+    // The resumable form wins everywhere (the wave shades its finished lanes once at most 12/64
     // still walk), and so do persistent waves pulling tiles from a cursor (variants 30/34: +6% on
     // the 484-object scene, +11% on 100k objects over the one-tile-per-wave grid, variants 28/26).
     const size_t cbBytes = 4 * (size_t)ctx->cnodeCount * sizeof(float4);
