@@ -93,6 +93,7 @@ typedef struct pt_render_stats {
     uint64_t cycles_leaf_tests;
     uint64_t cycles_shading;
     uint64_t cycles_total;
+    uint64_t cycles_lane_idle;  /* resumable variants: lane cycles spent done while the tile still ran */
 } pt_render_stats;
 
 typedef struct pt_context pt_context;

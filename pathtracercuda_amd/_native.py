@@ -42,7 +42,8 @@ class PtRenderStats(C.Structure):
                 ("sky_lookups", C.c_uint64), ("segments", C.c_uint64), ("samples", C.c_uint64),
                 ("wave_node_iters", C.c_uint64), ("wave_prim_iters", C.c_uint64), ("wave_hits", C.c_uint64),
                 ("wave_sky", C.c_uint64), ("wave_segments", C.c_uint64), ("cycles_node_walk", C.c_uint64),
-                ("cycles_leaf_tests", C.c_uint64), ("cycles_shading", C.c_uint64), ("cycles_total", C.c_uint64)]
+                ("cycles_leaf_tests", C.c_uint64), ("cycles_shading", C.c_uint64), ("cycles_total", C.c_uint64),
+                ("cycles_lane_idle", C.c_uint64)]
 
 
 # symbol -> (restype, argtypes); the CPU test suite checks that every declaration in include/*.h

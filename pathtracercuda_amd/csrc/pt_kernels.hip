@@ -224,6 +224,7 @@ struct Counters {
     uint32_t w_node, w_prim, w_hits, w_sky, w_segments;
     // wave-level shader-clock cycles per phase (instrumented variant only)
     uint64_t cyc_node, cyc_leaf, cyc_shade, cyc_total;
+    uint64_t cyc_lane_idle;     // per lane: cycles between finishing its pixel and the tile's end
 };
 
 // Adds the cycles since `t0` to `acc` once per wave and restarts the stamp.
@@ -1052,6 +1053,7 @@ PT_DEV void flush_counters(const TraceParams& P, const Counters& cnt)
     atomicAdd(&P.stats[12], (unsigned long long)cnt.cyc_leaf);
     atomicAdd(&P.stats[13], (unsigned long long)cnt.cyc_shade);
     atomicAdd(&P.stats[14], (unsigned long long)cnt.cyc_total);
+    atomicAdd(&P.stats[15], (unsigned long long)cnt.cyc_lane_idle);
 }
 
 // One atomic per wave: the first active lane adds n to *cursor and broadcasts the old value.
@@ -1163,6 +1165,7 @@ __global__ void __launch_bounds__(WPB * 64, MINW) trace_kernel(TraceParams P)
         const float fx = (float)(int32_t)pc.px, fy = (float)(int32_t)pc.py;
         camera_ray(P, fx, fy, rng, ps.o, ps.d);
         uint64_t tAll = STATS ? __builtin_amdgcn_s_memtime() : 0;
+        uint64_t tDone = 0;
         if (WW >= 100) {
             bool fresh = true;
             TravState ts = {0u, 0u, 0xffffffffu, kFltMax};
@@ -1175,6 +1178,7 @@ __global__ void __launch_bounds__(WPB * 64, MINW) trace_kernel(TraceParams P)
                 uint64_t tS = STATS ? __builtin_amdgcn_s_memtime() : 0;
                 if (shade<STATS>(P, prims, ts.elem, ts.tMax, ps, rng, cnt)) finish_path<STATS>(P, ps, rng, fx, fy, cnt);
                 if (STATS) wave_time(cnt.cyc_shade, tS);
+                if (STATS && !ps.alive) tDone = __builtin_amdgcn_s_memtime();
             }
         }
         while (WW < 100 && ps.alive) {
@@ -1187,6 +1191,7 @@ __global__ void __launch_bounds__(WPB * 64, MINW) trace_kernel(TraceParams P)
             if (shade<STATS>(P, prims, e, t, ps, rng, cnt)) finish_path<STATS>(P, ps, rng, fx, fy, cnt);
             if (STATS) wave_time(cnt.cyc_shade, tS);
         }
+        if (STATS && WW >= 100 && tDone) cnt.cyc_lane_idle += __builtin_amdgcn_s_memtime() - tDone;
         if (STATS) wave_time(cnt.cyc_total, tAll);
         store_pixel(P, pc, rng, ps);
     }
@@ -1903,6 +1908,7 @@ static int render_impl(pt_context* ctx, const pt_camera* cam, uint32_t spp, uint
         stats->cycles_leaf_tests = h[12];
         stats->cycles_shading = h[13];
         stats->cycles_total = h[14];
+        stats->cycles_lane_idle = h[15];
     }
     return PT_OK;
 }

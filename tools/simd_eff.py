@@ -14,13 +14,15 @@ ap.add_argument("--scene", default=str(ROOT / "scenes/generated_scene.scene.json
 ap.add_argument("--width", type=int, default=1920)
 ap.add_argument("--height", type=int, default=1080)
 ap.add_argument("--variants", default="1,3")
+ap.add_argument("--spp", type=int, default=8)
+ap.add_argument("--chunks", type=int, default=1)
 a = ap.parse_args()
 pt = pa.Pathtracer(a.width, a.height)
 cam = pt.load_scene(a.scene)
 res = {}
 for v in [int(x) for x in a.variants.split(",")]:
     pt.set_kernel_variant(v)
-    st = pt.render_instrumented(cam, 8, 1, True)
+    st = pt.render_instrumented(cam, a.spp, a.chunks, True)
     eff = {k: round(st[l] / (64.0 * st[w]), 3) if st[w] else None for k, l, w in [
         ("node", "node_tests", "wave_node_iters"), ("prim", "prim_tests", "wave_prim_iters"),
         ("hit_shade", "hits", "wave_hits"), ("sky", "sky_lookups", "wave_sky"), ("segment", "segments", "wave_segments")]}
@@ -29,5 +31,6 @@ for v in [int(x) for x in a.variants.split(",")]:
     tot = st["cycles_total"] or 1
     shares = {k: round(st[k] / tot, 3) for k in ("cycles_node_walk", "cycles_leaf_tests", "cycles_shading")}
     res[v] = {"simd_efficiency": eff, "per_sample": per_sample, "cycle_share": shares,
-              "wave_cycles_per_sample": round(tot / st["samples"] * 64, 1)}
+              "wave_cycles_per_sample": round(tot / st["samples"] * 64, 1),
+              "lane_idle_after_pixel_done": round(st["cycles_lane_idle"] / (64.0 * tot), 3)}
 print(json.dumps({"scene": pathlib.Path(a.scene).name, "variants": res}, indent=1))
