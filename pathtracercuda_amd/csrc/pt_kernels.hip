@@ -457,13 +457,14 @@ PT_DEV float slab_lo_x(const SlabRay& R, f2v bx, f2v by, f2v bz, float tMin, flo
 }
 
 // Both children of interior record `cur`, in the reference's visit order (trace.cu:66-77: near =
-// second child when the ray direction is negative along the split axis).  The slab values are
-// put in near/far order first so that each hit flag comes straight from compares (a wave mask)
-// rather than from selects between flags, which the compiler materialises per lane.
+// second child when the ray direction is negative along the split axis).  Only the choice of
+// the next node and of the pushed (far) child depends on the order: "both hit" and "any hit" are
+// symmetric, so the hit flags stay compare results (wave masks, combined on the SALU) and three
+// selects pick the next node, the far node and its entry distance.
 struct ChildPair {
-    bool hN, hF;
-    uint32_t wN, wF;
-    float loN, loF;
+    bool both, any;             // both children hit / at least one does
+    uint32_t wNext, wF;         // next node (the near one when both hit), far node (pushed when both hit)
+    float loNext, loF;          // their slab entry distances
 };
 
 PT_DEV ChildPair cb_children(const float4* __restrict__ cnodes, uint32_t cur, const SlabRay& R, uint32_t negMask,
@@ -476,14 +477,16 @@ PT_DEV ChildPair cb_children(const float4* __restrict__ cnodes, uint32_t cur, co
     const float loR = slab_lo_x(R, f2(Q2.x, Q2.y), f2(Q2.z, Q2.w), f2(Q1.z, Q1.w), tMin, XR);
     const bool isNeg = (negMask & __float_as_uint(Q3.z)) != 0u;
     const uint32_t wL = __float_as_uint(Q3.x), wR = __float_as_uint(Q3.y);
+    const bool hL = XL > loL && tMax > loL;
+    const bool hR = XR > loR && tMax > loR;
+    const bool takeL = hL && (!hR || !isNeg);
     ChildPair c;
-    c.loN = isNeg ? loR : loL;
-    c.loF = isNeg ? loL : loR;
-    const float XN = isNeg ? XR : XL, XF = isNeg ? XL : XR;
-    c.hN = XN > c.loN && tMax > c.loN;
-    c.hF = XF > c.loF && tMax > c.loF;
-    c.wN = isNeg ? wR : wL;
+    c.both = hL && hR;
+    c.any = hL || hR;
+    c.wNext = takeL ? wL : wR;
+    c.loNext = takeL ? loL : loR;
     c.wF = isNeg ? wL : wR;
+    c.loF = isNeg ? loL : loR;
     return c;
 }
 
@@ -525,12 +528,12 @@ PT_DEV uint32_t traverse_cb(const float4* __restrict__ cnodes, const float4* __r
         while ((cur >> 24) == 0u) {                               // interior walk
             if (STATS) { cnt.node_tests += 2; wave_tick(cnt.w_node); }
             const ChildPair ch = cb_children(cnodes, cur, R, negMask, tMin, tMax);   // trace.cu:66-77
-            if (ch.hN && ch.hF) {
+            if (ch.both) {
                 stack[64u * sp] = make_uint2(ch.wF, __float_as_uint(ch.loF));
                 ++sp;
             }
-            if (ch.hN || ch.hF) {
-                cur = ch.hN ? ch.wN : ch.wF;
+            if (ch.any) {
+                cur = ch.wNext;
             } else if (!pop()) {
                 done = true;
                 break;
@@ -614,12 +617,12 @@ PT_DEV bool traverse_cb_phase(const float4* __restrict__ cnodes, const float4* _
         while ((cur >> 24) == 0u) {                               // interior walk
             if (STATS) { cnt.node_tests += 2; wave_tick(cnt.w_node); }
             const ChildPair ch = cb_children(cnodes, cur, R, negMask, tMin, tMax);   // trace.cu:66-77
-            if (ch.hN && ch.hF) {
+            if (ch.both) {
                 stack[64u * sp] = make_uint2(ch.wF, __float_as_uint(ch.loF));
                 ++sp;
             }
-            if (ch.hN || ch.hF) {
-                cur = ch.hN ? ch.wN : ch.wF;
+            if (ch.any) {
+                cur = ch.wNext;
             } else if (!pop()) {
                 done = true;
                 break;
@@ -710,13 +713,13 @@ PT_DEV uint32_t traverse_spec(const float4* __restrict__ cnodes, const float4* _
                 } else {
                     if (STATS) { cnt.node_tests += 2; wave_tick(cnt.w_node); }
                     const ChildPair ch = cb_children(cnodes, cur, R, negMask, tMin, tMax);
-                    if (ch.hN && ch.hF) {
+                    if (ch.both) {
                         stack[64u * sp] = make_uint2(ch.wF, __float_as_uint(ch.loF));
                         ++sp;
                     }
-                    if (ch.hN || ch.hF) {
-                        cur = ch.hN ? ch.wN : ch.wF;
-                        curLo = ch.hN ? ch.loN : ch.loF;
+                    if (ch.any) {
+                        cur = ch.wNext;
+                        curLo = ch.loNext;
                     } else {
                         done = true;
                         while (sp > 0) {
