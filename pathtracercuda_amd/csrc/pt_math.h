@@ -27,8 +27,9 @@ constexpr float kFltMax = 3.402823466e+38f;
 // Correctly rounded 1/x and sqrt(x) in fewer VALU instructions than hipcc's general expansions.
 // tools/fp_exhaustive.hip checks every one of the 2^32 inputs on gfx950: v_rcp_f32 followed by one
 // fma Newton step equals the correctly rounded reciprocal for 2^-125 <= |x| <= 2^125, and
-// v_sqrt_f32 followed by the +-1 ulp fma residual correction equals the correctly rounded square
-// root for 2^-96 <= x <= FLT_MAX (profiles/r01_fp_exhaustive.json: 0 mismatches).  Other inputs
+// v_rsq_f32 followed by one Newton correction of x * rsq(x) with the exact fma residual
+// (5 VALU; the v_sqrt_f32 + +-1 ulp residual test it replaces took 9) equals the correctly rounded
+// square root for 2^-96 <= x <= FLT_MAX (profiles/r01_fp_exhaustive.json: 0 mismatches).  Other inputs
 // (zero, denormals, huge values, inf, NaN) take the general path.  Being correctly rounded, both
 // give exactly IEEE 1/x and sqrt(x) -- the oracle's and the reference's values.
 PT_DEV float rcp_rn(float x)
@@ -44,12 +45,12 @@ PT_DEV float rcp_rn(float x)
 
 PT_DEV float sqrt_rn(float x)
 {
-    if (x >= 0x1p-96f && x <= 3.40282347e+38f) {
-        const float s = __builtin_amdgcn_sqrtf(x);
-        const float sm = __uint_as_float(__float_as_uint(s) - 1u), sp = __uint_as_float(__float_as_uint(s) + 1u);
-        const float rm = __builtin_fmaf(-sm, s, x), rp = __builtin_fmaf(-sp, s, x);
-        const float r = rm <= 0.0f ? sm : s;
-        return rp > 0.0f ? sp : r;
+    // one unsigned compare: 2^-96 <= x <= FLT_MAX (negatives, inf and NaN fall outside)
+    if (__float_as_uint(x) - 0x0f800000u <= 0x7f7fffffu - 0x0f800000u) {
+        const float y = __builtin_amdgcn_rsqf(x);          // ~1/sqrt(x)
+        const float s0 = x * y, h = 0.5f * y;
+        const float r = __builtin_fmaf(-s0, s0, x);        // exact residual x - s0^2
+        return __builtin_fmaf(r, h, s0);
     }
     return sqrtf(x);
 }

@@ -154,7 +154,7 @@ def test_fast_reciprocal_and_sqrt_exhaustive(gpu_available, root):
     assert res["sqrt_rn"]["mismatches"] == 0, res["sqrt_rn"]
     # the guards matter: the raw sequences are not correctly rounded everywhere
     assert res["diag_rcp_newton_unguarded"]["mismatches"] > 0
-    assert res["diag_sqrt_corrected_unguarded"]["mismatches"] > 0
+    assert res["diag_sqrt_rsq_newton_unguarded"]["mismatches"] > 0
 
 
 def test_progressive_frames_with_camera_moves(gpu_available, scenes):
