@@ -431,9 +431,10 @@ struct SlabRay {
 };
 
 // lo and X of one box (see above); the fast form under the same conditions as node_test_fast.
+template <bool ALLFAST = false>
 PT_DEV float slab_lo_x(const SlabRay& R, f2v bx, f2v by, f2v bz, float tMin, float& X)
 {
-    if (R.fast) {
+    if (ALLFAST || R.fast) {
         const f2v tx = (bx - R.ox2) * R.ix2;
         const f2v ty = (by - R.oy2) * R.iy2;
         const f2v tz = (bz - R.oz2) * R.iz2;
@@ -467,14 +468,15 @@ struct ChildPair {
     float loNext, loF;          // their slab entry distances
 };
 
+template <bool ALLFAST = false>
 PT_DEV ChildPair cb_children(const float4* __restrict__ cnodes, uint32_t cur, const SlabRay& R, uint32_t negMask,
                              float tMin, float tMax)
 {
     const float4 Q0 = cnodes[4 * cur], Q1 = cnodes[4 * cur + 1];
     const float4 Q2 = cnodes[4 * cur + 2], Q3 = cnodes[4 * cur + 3];
     float XL, XR;
-    const float loL = slab_lo_x(R, f2(Q0.x, Q0.y), f2(Q0.z, Q0.w), f2(Q1.x, Q1.y), tMin, XL);
-    const float loR = slab_lo_x(R, f2(Q2.x, Q2.y), f2(Q2.z, Q2.w), f2(Q1.z, Q1.w), tMin, XR);
+    const float loL = slab_lo_x<ALLFAST>(R, f2(Q0.x, Q0.y), f2(Q0.z, Q0.w), f2(Q1.x, Q1.y), tMin, XL);
+    const float loR = slab_lo_x<ALLFAST>(R, f2(Q2.x, Q2.y), f2(Q2.z, Q2.w), f2(Q1.z, Q1.w), tMin, XR);
     const bool isNeg = (negMask & __float_as_uint(Q3.z)) != 0u;
     const uint32_t wL = __float_as_uint(Q3.x), wR = __float_as_uint(Q3.y);
     const bool hL = XL > loL && tMax > loL;
@@ -488,6 +490,36 @@ PT_DEV ChildPair cb_children(const float4* __restrict__ cnodes, uint32_t cur, co
     c.wF = isNeg ? wL : wR;
     c.loF = isNeg ? loL : loR;
     return c;
+}
+
+// The interior walk of the resumable traversal (trace.cu:66-77 per visited node): descend until a
+// leaf is reached (returns false, cur = leaf word) or the stack holds no entry that passes its
+// re-test (returns true).  Written for few exec-mask operations (the CU's one scalar unit serves
+// all its waves): ALLFAST (wave-uniform, decided by the caller) drops the per-lane exact-form
+// branch of the slab test, and the far child is written to the stack unconditionally -- the slot
+// above the top, inside the lane's column since an interior node has at most depth - 2 pending
+// entries -- with the stack pointer advanced only when both children are hit.
+template <bool STATS, bool ALLFAST>
+PT_DEV bool walk_interior(const float4* __restrict__ cnodes, uint2* stack, const SlabRay& R, uint32_t negMask,
+                          float tMin, float tMax, uint32_t& cur, uint32_t& sp, Counters& cnt)
+{
+    while ((cur >> 24) == 0u) {
+        if (STATS) { cnt.node_tests += 2; wave_tick(cnt.w_node); }
+        const ChildPair ch = cb_children<ALLFAST>(cnodes, cur, R, negMask, tMin, tMax);
+        stack[64u * sp] = make_uint2(ch.wF, __float_as_uint(ch.loF));
+        sp += ch.both ? 1u : 0u;
+        if (ch.any) {
+            cur = ch.wNext;
+        } else {
+            bool found = false;
+            while (sp > 0) {
+                const uint2 e = stack[64u * (--sp)];
+                if (tMax > __uint_as_float(e.y)) { cur = e.x; found = true; break; }
+            }
+            if (!found) return true;
+        }
+    }
+    return false;
 }
 
 template <bool STATS>
@@ -572,7 +604,7 @@ struct TravState {
     float tMax;
 };
 
-template <bool STATS, int EXITQ>
+template <bool STATS, int EXITQ, bool LEAN = false>
 PT_DEV bool traverse_cb_phase(const float4* __restrict__ cnodes, const float4* __restrict__ prims, uint2* stack,
                               const TraceParams& P, f3 o, f3 d, bool fresh, TravState& ts, Counters& cnt)
 {
@@ -613,7 +645,12 @@ PT_DEV bool traverse_cb_phase(const float4* __restrict__ cnodes, const float4* _
         return false;
     };
     uint64_t tPhase = STATS ? __builtin_amdgcn_s_memtime() : 0;
+    const bool allFast = LEAN && __ballot(!R.fast) == 0;          // wave-uniform
     while (!done) {
+        if (LEAN) {
+            done = allFast ? walk_interior<STATS, true>(cnodes, stack, R, negMask, tMin, tMax, cur, sp, cnt)
+                           : walk_interior<STATS, false>(cnodes, stack, R, negMask, tMin, tMax, cur, sp, cnt);
+        } else {
         while ((cur >> 24) == 0u) {                               // interior walk
             if (STATS) { cnt.node_tests += 2; wave_tick(cnt.w_node); }
             const ChildPair ch = cb_children(cnodes, cur, R, negMask, tMin, tMax);   // trace.cu:66-77
@@ -627,6 +664,7 @@ PT_DEV bool traverse_cb_phase(const float4* __restrict__ cnodes, const float4* _
                 done = true;
                 break;
             }
+        }
         }
         if (STATS) wave_time(cnt.cyc_node, tPhase);
         if (done) break;
@@ -1174,7 +1212,7 @@ __global__ void __launch_bounds__(WPB * 64, MINW) trace_kernel(TraceParams P)
             TravState ts = {0u, 0u, 0xffffffffu, kFltMax};
             while (ps.alive) {
                 if (STATS && fresh) { cnt.segments++; wave_tick(cnt.w_segments); }
-                const bool tdone = traverse_cb_phase<STATS, WW - 100>(nodes, prims, reinterpret_cast<uint2*>(stack), P,
+                const bool tdone = traverse_cb_phase<STATS, WW % 100, (WW >= 200)>(nodes, prims, reinterpret_cast<uint2*>(stack), P,
                                                                         ps.o, ps.d, fresh, ts, cnt);
                 fresh = tdone;
                 if (!tdone) continue;                              // suspended: resumes next round
@@ -1530,6 +1568,8 @@ static hipError_t launch_variant(int v, const TraceParams& P, hipStream_t stream
     case 37: return launch_one<STATS, 1, 4, 120, 5, true>(P, stream);
     case 38: return launch_one<STATS, 1, 4, 116, 5, true>(P, stream);
     case 39: return launch_one<STATS, 0, 4, 116, 5, true>(P, stream);
+    case 40: return launch_one<STATS, 1, 4, 212, 5, true>(P, stream);     // lean interior walk
+    case 41: return launch_one<STATS, 0, 4, 212, 5, true>(P, stream);
     default: return launch_one<STATS, 0, 4, 1, 1>(P, stream);
     }
 }
@@ -1546,7 +1586,7 @@ static int pick_variant(const pt_context* ctx)
     // still walk), and so do persistent waves pulling tiles from a cursor (variants 30/34: +6% on
     // the 484-object scene, +11% on 100k objects over the one-tile-per-wave grid, variants 28/26).
     const size_t cbBytes = 4 * (size_t)ctx->cnodeCount * sizeof(float4);
-    if (ctx->cnodes) return cbBytes <= 48 * 1024 ? 30 : 34;
+    if (ctx->cnodes) return cbBytes <= 48 * 1024 ? 40 : 41;
     const size_t nodeBytes = 2 * (size_t)ctx->nodeCount * sizeof(float4);
     return nodeBytes <= 48 * 1024 ? 6 : 4;
 }
@@ -2015,7 +2055,7 @@ PT_API uint32_t pt_local_rows(const pt_context* ctx) { return ctx ? ctx->rows : 
 
 PT_API int pt_set_kernel_variant(pt_context* ctx, int variant)
 {
-    if (!ctx || variant < 0 || variant > 39) return PT_ERR_ARG;
+    if (!ctx || variant < 0 || variant > 41) return PT_ERR_ARG;
     ctx->variant = variant;
     return PT_OK;
 }
