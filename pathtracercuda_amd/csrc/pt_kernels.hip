@@ -218,6 +218,87 @@ PT_DEV bool prim_hit(const float4* __restrict__ prims, uint32_t p, f3 o, f3 d, f
     return true;
 }
 
+// prim_hit for mixed-type leaves, written for the scalar unit: each shape family present among the
+// wave's active lanes is evaluated for all of them behind a wave-uniform branch, and each lane
+// selects its own family's verdict.  A lane's arithmetic is prim_hit's, operation for operation;
+// the reject tests are the same comparisons, negated (so NaNs pass or fail exactly as there), and
+// lanes of other families only compute values that are discarded.  The wave issues the same VALU
+// for the families present, without a divergent if/else (exec save, flip, restore on the CU's one
+// scalar unit) per family, per guard and per test.
+PT_DEV bool prim_hit_u(const float4* __restrict__ prims, uint32_t p, f3 o, f3 d, float tMin, float tMax, float& tOut,
+                       bool act = true)     // act = false: the lane joins no family (its verdict is discarded)
+{
+    const float4 r0 = prims[4 * p + 0];
+    const float4 r1 = prims[4 * p + 1];
+    const float4 r2 = prims[4 * p + 2];
+    const uint32_t type = __float_as_uint(prims[4 * p + 3].x);
+    const LocalRay r = to_local(r0, r1, r2, o, d);
+    const bool planar = act & (type == DISK || type == QUAD);   // lanes with act = false join no family
+    const bool cube = act & (type == CUBE);
+    const bool quadric = act & (type != DISK) & (type != QUAD) & (type != CUBE);
+    bool hit = false;
+    float t = 0.0f;
+    if (__ballot(planar) != 0ull) {                         // Hittable.inl:205-235, 299-329
+        const float tp = -r.o.y / r.d.y;
+        const float hx = r.o.x + r.d.x * tp;
+        const float hz = r.o.z + r.d.z * tp;
+        const bool inQuad = !(fabsf(hx) > 1.0f || fabsf(hz) > 1.0f);
+        const bool inDisk = !((hx * hx + hz * hz) >= 1.0f);
+        const bool hp = planar & !(r.d.y == 0.0f) & !(tp <= tMin || tp > tMax) & (type == QUAD ? inQuad : inDisk);
+        t = hp ? tp : t;
+        hit = hp;
+    }
+    if (__ballot(cube) != 0ull) {                           // Hittable.inl:331-358, AABB.inl:46-69
+        float lo = tMin, hi = tMax;
+        const float ox[3] = {r.o.x, r.o.y, r.o.z};
+        const float dx[3] = {r.d.x, r.d.y, r.d.z};
+#pragma unroll
+        for (int a = 0; a < 3; ++a) {
+            const float invD = rcp_rn_u(dx[a]);
+            const float t0 = (-1.0f - ox[a]) * invD;
+            const float t1 = (1.0f - ox[a]) * invD;
+            const bool sw = invD < 0.0f;
+            const float n0 = sw ? t1 : t0, n1 = sw ? t0 : t1;
+            lo = n0 > lo ? n0 : lo;
+            hi = n1 < hi ? n1 : hi;
+        }
+        const bool hc = cube & !(hi <= lo);
+        t = hc ? lo : t;
+        hit = hit | hc;
+    }
+    if (__ballot(quadric) != 0ull) {                        // quadric_roots + Hittable.inl:147-297
+        const float B = (type == SPHERE) ? 1.0f : (type == CONE ? -1.0f : 0.0f);
+        const float Hc = (type == PARABOLOID) ? -1.0f : 0.0f;
+        const float J = (type == SPHERE || type == CYLINDER) ? -1.0f : 0.0f;
+        const f3 ro = r.o, rd = r.d;
+        const float a = (rd.x * rd.x + (B * rd.y) * rd.y) + rd.z * rd.z;
+        const float b = (((2.0f * ro.x) * rd.x + ((2.0f * B) * ro.y) * rd.y) + (2.0f * ro.z) * rd.z) + Hc * rd.y;
+        const float c = (((ro.x * ro.x + (B * ro.y) * ro.y) + ro.z * ro.z) + Hc * ro.y) + J;
+        const float disc = b * b - 4.0f * a * c;
+        const bool real = !(disc < 0.0f);
+        if (__ballot(quadric & real) != 0ull) {              // most tests end here: no real root
+        const float rt = sqrt_rn_u(real ? disc : 1.0f);     // discarded where !real
+        const float q = b < 0.0f ? -0.5f * (b - rt) : -0.5f * (b + rt);
+        const float x0 = q / a;
+        const float x1 = c / q;
+        const float t0 = x0 > x1 ? x1 : x0;
+        const float t1 = x0 > x1 ? x0 : x1;
+        const bool pass = quadric & real & !(t0 > tMax || t1 <= tMin);
+        const float h0 = rd.y * t0 + ro.y;
+        const float h1 = rd.y * t1 + ro.y;
+        const bool v0 = (t0 > tMin) & (t0 <= tMax) & (h0 >= -1.0f) & (h0 <= 1.0f);
+        const bool v1 = (t1 > tMin) & (t1 <= tMax) & (h1 >= -1.0f) & (h1 <= 1.0f);
+        const bool sph = type == SPHERE;
+        const bool hq = pass & (sph | v0 | v1);
+        const float tq = sph ? (t0 > tMin ? t0 : t1) : (v0 ? t0 : t1);
+        t = hq ? tq : t;
+        hit = hit | hq;
+        }
+    }
+    tOut = t;
+    return hit;
+}
+
 struct Counters {
     uint32_t node_tests, prim_tests, hits, sky, segments, samples;
     // wave-level executions of the same points (SIMD efficiency = lane count / (64 * wave count))
@@ -604,7 +685,9 @@ struct TravState {
     float tMax;
 };
 
-template <bool STATS, int EXITQ, bool LEAN = false>
+// LEAN (WW = 100 * (LEAN + 1) + EXITQ): bit 0 -- walk_interior for the interior walk; bit 2 --
+// prim_hit_u (select form) for the primitive tests.  Results are identical for every LEAN.
+template <bool STATS, int EXITQ, int LEAN = 0>
 PT_DEV bool traverse_cb_phase(const float4* __restrict__ cnodes, const float4* __restrict__ prims, uint2* stack,
                               const TraceParams& P, f3 o, f3 d, bool fresh, TravState& ts, Counters& cnt)
 {
@@ -645,9 +728,9 @@ PT_DEV bool traverse_cb_phase(const float4* __restrict__ cnodes, const float4* _
         return false;
     };
     uint64_t tPhase = STATS ? __builtin_amdgcn_s_memtime() : 0;
-    const bool allFast = LEAN && __ballot(!R.fast) == 0;          // wave-uniform
+    const bool allFast = (LEAN & 1) && __ballot(!R.fast) == 0;          // wave-uniform
     while (!done) {
-        if (LEAN) {
+        if (LEAN & 1) {
             done = allFast ? walk_interior<STATS, true>(cnodes, stack, R, negMask, tMin, tMax, cur, sp, cnt)
                            : walk_interior<STATS, false>(cnodes, stack, R, negMask, tMin, tMax, cur, sp, cnt);
         } else {
@@ -672,7 +755,7 @@ PT_DEV bool traverse_cb_phase(const float4* __restrict__ cnodes, const float4* _
         while (leafCnt > 0) {
             if (STATS) { cnt.prim_tests++; wave_tick(cnt.w_prim); }
             float t;
-            if (prim_hit(prims, leafOff, o, d, tMin, tMax, t)) {
+            if ((LEAN & 4) ? prim_hit_u(prims, leafOff, o, d, tMin, tMax, t) : prim_hit(prims, leafOff, o, d, tMin, tMax, t)) {
                 tMax = t;
                 elem = leafOff;
             }
@@ -1212,7 +1295,7 @@ __global__ void __launch_bounds__(WPB * 64, MINW) trace_kernel(TraceParams P)
             TravState ts = {0u, 0u, 0xffffffffu, kFltMax};
             while (ps.alive) {
                 if (STATS && fresh) { cnt.segments++; wave_tick(cnt.w_segments); }
-                const bool tdone = traverse_cb_phase<STATS, WW % 100, (WW >= 200)>(nodes, prims, reinterpret_cast<uint2*>(stack), P,
+                const bool tdone = traverse_cb_phase<STATS, WW % 100, WW / 100 - 1>(nodes, prims, reinterpret_cast<uint2*>(stack), P,
                                                                         ps.o, ps.d, fresh, ts, cnt);
                 fresh = tdone;
                 if (!tdone) continue;                              // suspended: resumes next round
@@ -1570,6 +1653,8 @@ static hipError_t launch_variant(int v, const TraceParams& P, hipStream_t stream
     case 39: return launch_one<STATS, 0, 4, 116, 5, true>(P, stream);
     case 40: return launch_one<STATS, 1, 4, 212, 5, true>(P, stream);     // lean interior walk
     case 41: return launch_one<STATS, 0, 4, 212, 5, true>(P, stream);
+    case 42: return launch_one<STATS, 1, 4, 612, 5, true>(P, stream);     // + select-form primitive test
+    case 43: return launch_one<STATS, 0, 4, 612, 5, true>(P, stream);
     default: return launch_one<STATS, 0, 4, 1, 1>(P, stream);
     }
 }
@@ -2055,7 +2140,7 @@ PT_API uint32_t pt_local_rows(const pt_context* ctx) { return ctx ? ctx->rows : 
 
 PT_API int pt_set_kernel_variant(pt_context* ctx, int variant)
 {
-    if (!ctx || variant < 0 || variant > 41) return PT_ERR_ARG;
+    if (!ctx || variant < 0 || variant > 43) return PT_ERR_ARG;
     ctx->variant = variant;
     return PT_OK;
 }

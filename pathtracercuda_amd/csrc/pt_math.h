@@ -55,6 +55,38 @@ PT_DEV float sqrt_rn(float x)
     return sqrtf(x);
 }
 
+// The same values with the guard as a wave-uniform branch: the fast sequence runs for every
+// active lane, and only when some lane is outside the guard range does the wave evaluate the
+// general expression (for all its lanes) and select it there.  A divergent if/else costs the
+// scalar unit -- one per CU, shared by all its waves -- an exec-mask save, flip and restore per
+// call; this form costs one compare-to-mask and one scalar branch.
+PT_DEV float rcp_rn_u(float x)
+{
+    const float y = __builtin_amdgcn_rcpf(x);
+    const float e = __builtin_fmaf(-x, y, 1.0f);
+    float r = __builtin_fmaf(e, y, y);
+    const float ax = __builtin_fabsf(x);
+    const bool ok = ax >= 0x1p-125f && ax <= 0x1p125f;
+    if (__ballot(!ok) != 0ull) {
+        const float g = 1.0f / x;
+        r = ok ? r : g;
+    }
+    return r;
+}
+
+PT_DEV float sqrt_rn_u(float x)
+{
+    const float y = __builtin_amdgcn_rsqf(x);
+    const float s0 = x * y, h = 0.5f * y;
+    float s = __builtin_fmaf(__builtin_fmaf(-s0, s0, x), h, s0);
+    const bool ok = __float_as_uint(x) - 0x0f800000u <= 0x7f7fffffu - 0x0f800000u;
+    if (__ballot(!ok) != 0ull) {
+        const float g = sqrtf(x);
+        s = ok ? s : g;
+    }
+    return s;
+}
+
 // x / c for the constants c = PI, 2 PI: q = x * RN(1/c) corrected once with the exact residual
 // fma(-c, q, x) (Markstein), behind the guard 2^-100 <= |x| <= 2^100 (other inputs, incl. 0,
 // inf and NaN, divide).  Checked against the correctly rounded quotient for all 2^32 inputs by

@@ -10,7 +10,7 @@
 
 #include "../pathtracercuda_amd/csrc/pt_math.h"
 
-#define NSEQ 8
+#define NSEQ 10
 __device__ unsigned long long g_bad[NSEQ];
 __device__ uint32_t g_first[NSEQ][8];
 
@@ -49,6 +49,9 @@ __global__ void check(uint32_t base)
     // x / pi and x / (2 pi) (the sky's theta / PI, phi / (2 PI), the cosine pdf z / PI)
     check_one(6, same(pt::div_pi(x), x / pt::kPi), xb);
     check_one(7, same(pt::div_two_pi(x), x / pt::kTwoPi), xb);
+    // the wave-uniform-guard forms (pt_math.h *_u) used by the select-form primitive test
+    check_one(8, same(pt::rcp_rn_u(x), ref_rcp), xb);
+    check_one(9, same(pt::sqrt_rn_u(x), ref_sqrt), xb);
 }
 
 int main()
@@ -64,7 +67,8 @@ int main()
     if (hipMemcpyFromSymbol(bad, HIP_SYMBOL(g_bad), sizeof(bad)) != hipSuccess) return 2;
     if (hipMemcpyFromSymbol(first, HIP_SYMBOL(g_first), sizeof(first)) != hipSuccess) return 2;
     const char* names[NSEQ] = {"rcp_rn", "sqrt_rn", "diag_rcp_raw_all_inputs", "diag_rcp_newton_unguarded",
-                               "diag_sqrt_raw_all_inputs", "diag_sqrt_rsq_newton_unguarded", "div_pi", "div_two_pi"};
+                               "diag_sqrt_raw_all_inputs", "diag_sqrt_rsq_newton_unguarded", "div_pi", "div_two_pi",
+                               "rcp_rn_u", "sqrt_rn_u"};
     printf("{\n  \"inputs\": 4294967296,\n");
     for (int k = 0; k < NSEQ; ++k) {
         printf("  \"%s\": {\"mismatches\": %llu, \"first\": [", names[k], bad[k]);
