@@ -62,8 +62,10 @@ def algorithmic_bytes(stats: dict, pixels: int, launches: int) -> float:
 
 def load_pmc_traffic(workload: str):
     """Per-launch HBM bytes of the trace kernel from the committed rocprofv3 --pmc summary, and the
-    VALU issue fraction of the same launch: wave64 VALU instructions x 4 cycles (SIMD16) over
-    1024 SIMDs x shader-active cycles (GRBM_GUI_ACTIVE summed over the 8 XCDs)."""
+    issue utilisation of the same launch over shader-active cycles (GRBM_GUI_ACTIVE summed over the
+    8 XCDs): VALU = wave64 VALU instructions x 2 cycles (CDNA4 SIMD-32 throughput,
+    MI355X_MICROARCH.md cycle table) over 1024 SIMDs; SALU = scalar instructions per CU-cycle (one
+    scalar unit per CU, shared by its 4 SIMDs)."""
     for f in sorted((ROOT / "profiles").glob("*pmc_traffic*.json"), reverse=True):
         try:
             d = json.loads(f.read_text())
@@ -71,11 +73,14 @@ def load_pmc_traffic(workload: str):
             continue
         if d.get("workload") == workload and d.get("bytes_per_launch"):
             c = d.get("counters", {})
-            valu = None
-            if c.get("SQ_INSTS_VALU") and c.get("GRBM_GUI_ACTIVE"):
-                valu = round(4.0 * c["SQ_INSTS_VALU"] / (1024.0 * c["GRBM_GUI_ACTIVE"] / 8.0), 3)
-            return float(d["bytes_per_launch"]), f.name, valu
-    return None, None, None
+            util = {}
+            cyc = c.get("GRBM_GUI_ACTIVE", 0) / 8.0
+            if cyc and c.get("SQ_INSTS_VALU"):
+                util["valu_util"] = round(2.0 * c["SQ_INSTS_VALU"] / (1024.0 * cyc), 3)
+            if cyc and c.get("SQ_INSTS_SALU"):
+                util["salu_per_cu_cycle"] = round(c["SQ_INSTS_SALU"] / (256.0 * cyc), 3)
+            return float(d["bytes_per_launch"]), f.name, util
+    return None, None, {}
 
 
 def cpu_baseline(args, W, H):
@@ -184,7 +189,7 @@ def main():
     avg_launch_s = kernel_ms / args.steps / 1e3
     achieved = per_gpu_bytes / avg_launch_s / 1e9
     workload = f"generated_scene {W}x{H} {spp}spp chunk{chunk}"
-    traffic, traffic_src, valu_frac = load_pmc_traffic(workload)
+    traffic, traffic_src, util = load_pmc_traffic(workload)
     out = {
         "metric": "Msamples/sec + achieved HBM GB/s, 1080p 1024spp, 1/2/4/8 MI355X",
         "value": round(value, 3),
@@ -207,9 +212,9 @@ def main():
                      "bytes_per_sample": round(launch_bytes / (W * H * spp), 1),
                      "traffic_source": traffic_src,
                      # the algorithmic bytes are served from LDS and L2 (traffic = HBM bytes measured);
-                     # the kernel is bound by VALU issue, whose busy fraction the same profile gives
+                     # the kernel is issue/latency-bound: VALU and scalar-unit use from the same profile
                      "hbm_frac_measured": (round(traffic / avg_launch_s / 1e9 / HBM_PEAK_GBS, 5) if traffic else None),
-                     "valu_issue_frac": valu_frac},
+                     **util},
         "cpu_baseline": None,
     }
     if rank == 0 and n == 1 and args.cpu_baseline:
