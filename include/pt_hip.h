@@ -158,7 +158,7 @@ PT_API int pt_write_rng(pt_context *ctx, const uint32_t *src);
 
 PT_API uint32_t pt_local_rows(const pt_context *ctx);
 
-/* Tuning knob for A/B measurements: 0 = automatic (default); 1..43 select a trace-kernel variant
+/* Tuning knob for A/B measurements: 0 = automatic (default); 1..45 select a trace-kernel variant
  * (workgroup size, BVH/primitives staged in LDS or read through the caches, traversal loop shape,
  * occupancy target).  All variants produce bit-identical results. */
 PT_API int pt_set_kernel_variant(pt_context *ctx, int variant);

@@ -1651,10 +1651,12 @@ static hipError_t launch_variant(int v, const TraceParams& P, hipStream_t stream
     case 37: return launch_one<STATS, 1, 4, 120, 5, true>(P, stream);
     case 38: return launch_one<STATS, 1, 4, 116, 5, true>(P, stream);
     case 39: return launch_one<STATS, 0, 4, 116, 5, true>(P, stream);
-    case 40: return launch_one<STATS, 1, 4, 212, 5, true>(P, stream);     // lean interior walk
-    case 41: return launch_one<STATS, 0, 4, 212, 5, true>(P, stream);
+    case 40: return launch_one<STATS, 1, 4, 224, 5, true>(P, stream);     // lean interior walk, exit at <= 24/64
+    case 41: return launch_one<STATS, 0, 4, 212, 5, true>(P, stream);     // cache-read scene: exit at <= 12/64
     case 42: return launch_one<STATS, 1, 4, 612, 5, true>(P, stream);     // + select-form primitive test
     case 43: return launch_one<STATS, 0, 4, 612, 5, true>(P, stream);
+    case 44: return launch_one<STATS, 1, 4, 212, 5, true>(P, stream);     // lean walk, exit at <= 12/64
+    case 45: return launch_one<STATS, 0, 4, 224, 5, true>(P, stream);
     default: return launch_one<STATS, 0, 4, 1, 1>(P, stream);
     }
 }
@@ -2140,7 +2142,7 @@ PT_API uint32_t pt_local_rows(const pt_context* ctx) { return ctx ? ctx->rows : 
 
 PT_API int pt_set_kernel_variant(pt_context* ctx, int variant)
 {
-    if (!ctx || variant < 0 || variant > 43) return PT_ERR_ARG;
+    if (!ctx || variant < 0 || variant > 45) return PT_ERR_ARG;
     ctx->variant = variant;
     return PT_OK;
 }
