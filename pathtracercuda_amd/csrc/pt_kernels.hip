@@ -1657,6 +1657,7 @@ static hipError_t launch_variant(int v, const TraceParams& P, hipStream_t stream
     case 43: return launch_one<STATS, 0, 4, 612, 5, true>(P, stream);
     case 44: return launch_one<STATS, 1, 4, 212, 5, true>(P, stream);     // lean walk, exit at <= 12/64
     case 45: return launch_one<STATS, 0, 4, 224, 5, true>(P, stream);
+    case 46: return launch_one<STATS, 0, 4, 212, 4, true>(P, stream);     // deep cache-read BVH: LDS stacks allow 4 waves/SIMD, 128 VGPRs
     default: return launch_one<STATS, 0, 4, 1, 1>(P, stream);
     }
 }
@@ -1672,8 +1673,12 @@ static int pick_variant(const pt_context* ctx)
     // The resumable form wins everywhere (the wave shades its finished lanes once at most 12/64
     // still walk), and so do persistent waves pulling tiles from a cursor (variants 30/34: +6% on
     // the 484-object scene, +11% on 100k objects over the one-tile-per-wave grid, variants 28/26).
+    // A cache-read scene whose four LDS stacks per workgroup leave room for fewer than five
+    // workgroups per CU (BVH depth > 16) runs at 4 waves/SIMD anyway: variant 46 is variant 41
+    // compiled for that occupancy (128 VGPRs, no spill), +1% on the 100k-object scene (depth 19).
     const size_t cbBytes = 4 * (size_t)ctx->cnodeCount * sizeof(float4);
-    if (ctx->cnodes) return cbBytes <= 48 * 1024 ? 40 : 41;
+    const size_t stackBytes = 4 * (size_t)ctx->stackDepth * 64 * 8;
+    if (ctx->cnodes) return cbBytes <= 48 * 1024 ? 40 : (5 * stackBytes > 160 * 1024 ? 46 : 41);
     const size_t nodeBytes = 2 * (size_t)ctx->nodeCount * sizeof(float4);
     return nodeBytes <= 48 * 1024 ? 6 : 4;
 }
@@ -2142,7 +2147,7 @@ PT_API uint32_t pt_local_rows(const pt_context* ctx) { return ctx ? ctx->rows : 
 
 PT_API int pt_set_kernel_variant(pt_context* ctx, int variant)
 {
-    if (!ctx || variant < 0 || variant > 45) return PT_ERR_ARG;
+    if (!ctx || variant < 0 || variant > 46) return PT_ERR_ARG;
     ctx->variant = variant;
     return PT_OK;
 }

@@ -67,7 +67,7 @@ def test_render_bitexact(gpu_available, scenes, name, W, H, spp, chunks):
     assert pt.frames == ref.frames == chunks
 
 
-@pytest.mark.parametrize("variant", range(1, 46))
+@pytest.mark.parametrize("variant", range(1, 47))
 def test_every_kernel_variant_bitexact(gpu_available, scenes, variant):
     # all trace-kernel variants (schedules, LDS staging, occupancy) produce the reference's bits
     pt, cam, ref, osc = pair(scenes / "test_shapes.scene.json", 72, 40)
@@ -88,7 +88,7 @@ def test_persistent_variants_large_grid(gpu_available, scenes):
     pt.set_kernel_variant(1)
     pt.render(cam, 3, True, chunks=3)
     want = pt.accum().view(np.uint32).copy()       # bits: the reference's NaN pixels stay NaN
-    for variant in range(30, 46):
+    for variant in range(30, 47):
         pt.set_kernel_variant(variant)
         pt.set_rng_state(st)
         pt.render(cam, 3, True, chunks=3)
