@@ -895,8 +895,8 @@ PT_DEV Surface surface_of(const float4& r0, const float4& r1, const float4& r2, 
     case SPHERE:
         n = normalize(lp);
         if (needUV) {
-            const float theta = acos_(n.y);
-            const float phi = atan2_(n.z, n.x);
+            const float theta = acos_sel(n.y);
+            const float phi = atan2_sel(n.z, n.x);
             u = 1.0f - div_two_pi(phi);
             v = div_pi(theta);
         }
@@ -904,7 +904,7 @@ PT_DEV Surface surface_of(const float4& r0, const float4& r1, const float4& r2, 
     case CYLINDER:
         n = mk(lp.x, 0.0f, lp.z);
         if (needUV) {
-            const float phi = atan2_(n.z, n.x);
+            const float phi = atan2_sel(n.z, n.x);
             u = 1.0f - div_two_pi(phi);
             v = 1.0f - (lp.y * 0.5f + 0.5f);
         }
@@ -1027,8 +1027,8 @@ PT_DEV bool shade(const TraceParams& P, const float4* __restrict__ prims, uint32
         f3 sky = splat(0.0f);
         if (P.skybox != 0) {
             if (STATS) { cnt.sky++; wave_tick(cnt.w_sky); }
-            const float theta = acos_(ps.d.y);
-            const float phi = atan2_(ps.d.z, ps.d.x);
+            const float theta = acos_sel(ps.d.y);
+            const float phi = atan2_sel(ps.d.z, ps.d.x);
             const float v = div_pi(theta);
             const float u = div_two_pi(phi);
             sky = tex2d(P.textures[P.skybox - 1], u, v);

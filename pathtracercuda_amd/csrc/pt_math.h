@@ -222,6 +222,57 @@ PT_DEV float atan2_(float y, float x)
     return y < 0.0f ? -r : r;
 }
 
+// Select forms of acos_ and atan2_ for the kernel (sky lookup, sphere/cylinder uv): every lane
+// evaluates the operations of its own range -- the same operations in the same order as acos_ /
+// atan2_, so the same bits -- but the ranges are chosen by selects instead of divergent branches
+// (one sqrt with a per-lane operand, one polynomial), and the rare special inputs (NaN, zeros,
+// infinities, |x| > 1) overwrite the result afterwards in reverse order of precedence.
+PT_DEV float asin_core_le_half(float a)                  // asin_core for 0 <= a <= 0.5 (or NaN)
+{
+    const float z = a * a;
+    const float p = ((((4.2163199048E-2f * z + 2.4181311049E-2f) * z + 4.5470025998E-2f) * z + 7.4953002686E-2f) * z
+                     + 1.6666752422E-1f) * z * a + a;
+    return a < 1.0e-4f ? a : p;
+}
+
+PT_DEV float acos_sel(float x)
+{
+    const bool lo = x < -0.5f, hi = x > 0.5f;
+    const float s = sqrt_rn(0.5f * (lo ? (1.0f + x) : (1.0f - x)));
+    const float r = asin_core_le_half((lo || hi) ? s : fabsf(x));
+    float res = lo ? kPi - 2.0f * r : (hi ? 2.0f * r : (x < 0.0f ? kPio2 + r : kPio2 - r));
+    if (!(x >= -1.0f && x <= 1.0f)) res = (x != x) ? x : __uint_as_float(0x7fc00000u);
+    return res;
+}
+
+PT_DEV float atan_pos_sel(float x)
+{
+    const bool big = x > 2.414213562373095f;
+    const bool mid = !big && x > 0.4142135623730950f;
+    const float rb = -rcp_rn(x);
+    const float rm = (x - 1.0f) / (x + 1.0f);
+    const float y = big ? kPio2 : (mid ? kPio4 : 0.0f);
+    const float t = big ? rb : (mid ? rm : x);
+    const float z = t * t;
+    return y + ((((8.05374449538e-2f * z - 1.38776856032E-1f) * z + 1.99777106478E-1f) * z - 3.33329491539E-1f) * z * t + t);
+}
+
+PT_DEV float atan2_sel(float y, float x)
+{
+    const float ay = fabsf(y), ax = fabsf(x);
+    float r = atan_pos_sel(ay / ax);
+    r = x < 0.0f ? kPi - r : r;
+    r = y < 0.0f ? -r : r;
+    if (__builtin_isinf(ax)) {
+        const float q = __builtin_isinf(ay) ? ((x > 0.0f) ? kPio4 : 3.0f * kPio4) : ((x > 0.0f) ? 0.0f : kPi);
+        r = y < 0.0f ? -q : q;
+    }
+    if (x == 0.0f) r = y < 0.0f ? -kPio2 : kPio2;
+    if (y == 0.0f) r = (__float_as_uint(x) >> 31) ? ((__float_as_uint(y) >> 31) ? -kPi : kPi) : y;
+    if (x != x || y != y) r = x + y;
+    return r;
+}
+
 PT_DEV float log_(float x)
 {
     uint32_t b = __float_as_uint(x);

@@ -10,7 +10,7 @@
 
 #include "../pathtracercuda_amd/csrc/pt_math.h"
 
-#define NSEQ 10
+#define NSEQ 14
 __device__ unsigned long long g_bad[NSEQ];
 __device__ uint32_t g_first[NSEQ][8];
 
@@ -52,6 +52,14 @@ __global__ void check(uint32_t base)
     // the wave-uniform-guard forms (pt_math.h *_u) used by the select-form primitive test
     check_one(8, same(pt::rcp_rn_u(x), ref_rcp), xb);
     check_one(9, same(pt::sqrt_rn_u(x), ref_sqrt), xb);
+    // select forms of acos / atan (kernel sky lookup and uv) against the branchy forms the oracle
+    // restates: bit for bit, NaN payloads included; atan2 with every x in each argument position,
+    // paired with a hashed other argument (all bit patterns occur, specials included)
+    check_one(10, __float_as_uint(pt::acos_sel(x)) == __float_as_uint(pt::acos_(x)), xb);
+    check_one(11, __float_as_uint(pt::atan_pos_sel(x)) == __float_as_uint(pt::atan_pos(x)), xb);
+    const float h = __uint_as_float((xb * 2654435761u) ^ 0x9e3779b9u);
+    check_one(12, __float_as_uint(pt::atan2_sel(x, h)) == __float_as_uint(pt::atan2_(x, h)), xb);
+    check_one(13, __float_as_uint(pt::atan2_sel(h, x)) == __float_as_uint(pt::atan2_(h, x)), xb);
 }
 
 int main()
@@ -68,7 +76,7 @@ int main()
     if (hipMemcpyFromSymbol(first, HIP_SYMBOL(g_first), sizeof(first)) != hipSuccess) return 2;
     const char* names[NSEQ] = {"rcp_rn", "sqrt_rn", "diag_rcp_raw_all_inputs", "diag_rcp_newton_unguarded",
                                "diag_sqrt_raw_all_inputs", "diag_sqrt_rsq_newton_unguarded", "div_pi", "div_two_pi",
-                               "rcp_rn_u", "sqrt_rn_u"};
+                               "rcp_rn_u", "sqrt_rn_u", "acos_sel", "atan_pos_sel", "atan2_sel_y", "atan2_sel_x"};
     printf("{\n  \"inputs\": 4294967296,\n");
     for (int k = 0; k < NSEQ; ++k) {
         printf("  \"%s\": {\"mismatches\": %llu, \"first\": [", names[k], bad[k]);
