@@ -121,7 +121,25 @@ PT_DEV f3 divs(f3 v, float t) { return scale(rcp_rn(t), v); }
 PT_DEV float dot(f3 u, f3 v) { return u.x * v.x + u.y * v.y + u.z * v.z; }
 PT_DEV f3 cross(f3 u, f3 v) { return f3{u.y * v.z - u.z * v.y, u.z * v.x - u.x * v.z, u.x * v.y - u.y * v.x}; }
 PT_DEV float length(f3 v) { return sqrt_rn(v.x * v.x + v.y * v.y + v.z * v.z); }
-PT_DEV f3 normalize(f3 v) { return divs(v, length(v)); }
+// normalize = (1 / sqrt_rn(|v|^2)) * v with one range guard instead of two: when |v|^2 lies in
+// sqrt_rn's fast range [2^-96, FLT_MAX], the root lies in [2^-48, 2^64], inside rcp_rn's fast range,
+// so both fast sequences apply; otherwise both general paths run.  Same values as
+// divs(v, length(v)); one divergent region (exec-mask work on the scalar unit) fewer per call.
+PT_DEV f3 normalize(f3 v)
+{
+    const float l2 = v.x * v.x + v.y * v.y + v.z * v.z;
+    float inv;
+    if (__float_as_uint(l2) - 0x0f800000u <= 0x7f7fffffu - 0x0f800000u) {
+        const float y = __builtin_amdgcn_rsqf(l2);
+        const float s0 = l2 * y, h = 0.5f * y;
+        const float l = __builtin_fmaf(__builtin_fmaf(-s0, s0, l2), h, s0);
+        const float r = __builtin_amdgcn_rcpf(l);
+        inv = __builtin_fmaf(__builtin_fmaf(-l, r, 1.0f), r, r);
+    } else {
+        inv = rcp_rn(sqrtf(l2));
+    }
+    return scale(inv, v);
+}
 PT_DEV f3 reflect(f3 v, f3 n) { return sub(v, scale(2.0f * dot(v, n), n)); }
 PT_DEV f3 lerp(f3 x, f3 y, float a) { return add(scale(1.0f - a, x), scale(a, y)); }
 PT_DEV float clamp01(float x) { x = x < 0.0f ? 0.0f : x; x = x > 1.0f ? 1.0f : x; return x; }
