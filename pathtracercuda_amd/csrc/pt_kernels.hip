@@ -965,7 +965,7 @@ PT_DEV f3 vndf_sample_rsc(f3 V, float r, float s, float c, float a)
 {
     const f3 Vh = normalize(mk(a * V.x, a * V.y, V.z));
     const float lensq = Vh.x * Vh.x + Vh.y * Vh.y;
-    const f3 T1 = lensq > 0.0f ? scale(rcp_rn(sqrt_rn(lensq)), mk(-Vh.y, Vh.x, 0.0f)) : mk(1.0f, 0.0f, 0.0f);
+    const f3 T1 = lensq > 0.0f ? scale(rcp_sqrt_rn(lensq), mk(-Vh.y, Vh.x, 0.0f)) : mk(1.0f, 0.0f, 0.0f);
     const f3 T2 = cross(Vh, T1);
     const float t1 = r * c;
     float t2 = r * s;
@@ -988,8 +988,10 @@ PT_DEV float vndf_pdf(f3 H, f3 V, float a)    // MonteCarlo.h:104-114
 PT_DEV f3 specular_ggx(f3 F0, float NdotV, float NdotL, float NdotH, float VdotH, float a2)  // brdf.h:56-62
 {
     const float D = d_ggx(NdotH, a2);
-    const float lv = NdotL * sqrt_rn((-NdotV * a2 + NdotV) * NdotV + a2);   // brdf.h:18-24
-    const float ll = NdotV * sqrt_rn((-NdotL * a2 + NdotL) * NdotL + a2);
+    float sv, sl;                                                          // brdf.h:18-24
+    sqrt2_rn((-NdotV * a2 + NdotV) * NdotV + a2, (-NdotL * a2 + NdotL) * NdotL + a2, sv, sl);
+    const float lv = NdotL * sv;
+    const float ll = NdotV * sl;
     const float Vis = 0.5f / (lv + ll + 1e-5f);
     const float v = 1.0f - VdotH;                                          // brdf.h:27-32
     const float v2 = v * v;
