@@ -1087,16 +1087,17 @@ PT_DEV bool shade(const TraceParams& P, const float4* __restrict__ prims, uint32
     }
     float sn, cs;
     sincos_pos(kTwoPi * (specular ? rnd1 : rnd0), sn, cs);
-    const float sq = sqrt_rn(specular ? rnd0 : rnd1);
+    // sqrt of the lobe's radius uniform and the cosine lobe's sin(theta) behind one range guard
+    float sq, sinTheta;
+    sqrt2_rn(specular ? rnd0 : rnd1, 1.0f - rnd1, sq, sinTheta);
     if (mtype == 0u) {                                                        // LAMBERT (Material.inl:67-72)
-        dir = mk(cs * sqrt_rn(1.0f - rnd1), sn * sqrt_rn(1.0f - rnd1), sq);       // cosine_sample
+        dir = mk(cs * sinTheta, sn * sinTheta, sq);                            // cosine_sample
         pdf = div_pi(dir.z);
         att = scale(kInvPi, base);
     } else if (mtype <= 2u) {
         if (specular) {
             dir = reflect(neg(V), vndf_sample_rsc(V, sq, sn, cs, a));
         } else {
-            const float sinTheta = sqrt_rn(1.0f - rnd1);
             dir = mk(cs * sinTheta, sn * sinTheta, sq);
         }
         if (dir.z < 0.0f) {
