@@ -27,7 +27,7 @@ $(LIB):
 	mkdir -p $(LIB)
 
 $(LIB)/libpt_hip.so: $(SRC)/pt_kernels.hip $(SRC)/pt_math.h include/pt_hip.h | $(LIB)
-	$(HIPCC) $(HIPFLAGS) -shared -o $@ $(SRC)/pt_kernels.hip
+	$(HIPCC) $(HIPFLAGS) -shared -o $@ $(SRC)/pt_kernels.hip -lrccl
 
 $(LIB)/libpt_host.so: $(HOST_SRCS) $(HOST_HDRS) $(LIB)/libpt_hip.so
 	$(CXX) $(CXXFLAGS) -shared -o $@ $(HOST_SRCS) -L$(LIB) -lpt_hip -lz -Wl,-rpath,'$$ORIGIN'

@@ -1,23 +1,29 @@
-"""Benchmark: Msamples/s of the path-tracing hot path (BASELINE.json metric, config C3).
+"""Benchmark: Msamples/s of the path-tracing hot path (BASELINE.json metric).
 
-Workload (one "step"): generated_scene.json (484 quadrics + synthetic HDR sky) at 1920x1080,
-1024 spp as the reference's headless loop renders it -- 128 render() calls of 8 spp
-(main.cpp:272-279) -- executed as one chunked launch per GPU (bit-identical to 128 launches,
+Workloads (SURVEY.md §8 config labels; one "step" = one pass of the hot path over the workload):
+  C3 (default)  generated_scene.json (484 quadrics + synthetic HDR sky), 1920x1080, 1024 spp
+  C2            cornell_box.json, 512x512, 64 spp
+  C4            generated_scene.json, 3840x2160, 4096 spp
+  C5            100,490 random quadrics (tools/make_stress_scene.py, seeded), 1920x1080, 4096 spp
+Every workload runs as the reference's headless loop renders it -- render() calls of 8 spp
+(main.cpp:272-279) -- executed as one chunked launch per GPU (bit-identical to the call loop,
 tests/test_gpu_parity.py).  Inputs are resident on the GPU before the timed region (scene, BVH,
 sky texture, RNG state, accumulation buffer).
 
-N GPUs (torchrun, one process per GPU, RCCL): the image rows are interleaved over the ranks
-(row r -> rank r mod N), each rank renders its rows, and the HDR framebuffer is gathered to rank 0
-over RCCL inside the timed region.  Default weak scaling: each GPU keeps one 1080p frame's worth of
-pixels (the image grows by sqrt(N) per axis: 2720x1528, 3840x2160 (= C4), 5432x3056 at 1024 spp);
-`--scaling strong` renders the same 1080p image for every N.  A pixel's samples are one serial
-XORWOW stream, so strong scaling of a 1080p frame is bounded by its most expensive 8x8 tile
-(DESIGN.md "Multi-GPU"; tools/scale_sim.py).
+N GPUs (torch.distributed.run, one process per GPU, RCCL): the image is cut into 8-row bands,
+band b -> rank b mod N (pathtracercuda_amd/distributed.py), each rank renders its bands and the HDR
+framebuffer is gathered to rank 0 over RCCL inside the timed region.  Default: strong scaling (the
+same workload for every N); `--scaling weak` grows the image by sqrt(N) per axis instead.  At N > 1
+a short weak-scaling measurement is added as a secondary field; at N = 1 the C2 workload is added
+as a secondary record (`--secondary 0` turns both off).
 
-Printed JSON line (rank 0): value = samples of the whole image / step time; roofline = the trace
-kernel's algorithmic bytes (counted node/prim/material/sky reads + per-pixel
-state traffic, measured with the instrumented kernel on this workload) / its HIP-event time vs
-8.0 TB/s HBM; cpu_baseline = the oracle (CPU restatement) on a bounded sample of this workload.
+Printed JSON line (rank 0): value = samples of the whole workload / step time.  roofline: the
+trace kernel is bound by VALU issue -- achieved = its wave64 VALU instructions per
+launch (rocprofv3 PMC profile of the same workload, profiles/) / its live HIP-event launch time,
+peak = 1,024 SIMD-32 x 2.4 GHz / 2 cycles per wave64 instruction; traffic = measured HBM bytes per
+launch (same profile); the SURVEY §8(d) algorithmic bytes (served from LDS/L1/L2, not HBM) are
+reported as lds_l2_effective_GBs.  cpu_baseline = the oracle (CPU restatement, -O3) on every
+allowed core of this host, on a time-bounded sample of the same workload.
 """
 from __future__ import annotations
 
@@ -26,15 +32,28 @@ import json
 import math
 import os
 import pathlib
+import platform
 import sys
+import tempfile
 import time
 
 ROOT = pathlib.Path(__file__).resolve().parent
 sys.path.insert(0, str(ROOT))
 
-HBM_PEAK_GBS = 8000.0      # MI355X_MICROARCH.md: HBM3E 8.0 TB/s (spec)
+METRIC = "Msamples/sec + achieved HBM GB/s, 1080p 1024spp, 1/2/4/8 MI355X"
+HBM_PEAK_GBS = 8000.0                 # MI355X_MICROARCH.md: HBM3E 8.0 TB/s (spec)
+SIMDS, CLOCK_HZ = 1024, 2.4e9         # 256 CUs x 4 SIMD-32; max engine clock (MI355X_MICROARCH.md)
+VALU_PEAK_G = SIMDS * CLOCK_HZ / 2 / 1e9   # wave64 VALU instructions per second: 2 cycles each on SIMD-32
 NODE_B, PRIM_B, MAT_B, SKY_B = 32, 96, 40, 64            # SURVEY.md §8(d) per-event bytes
 PIXEL_STATE_B = 16 + 16 + 24 + 24                          # accum RMW + XORWOW state RMW, per pixel per launch
+CHUNK = 8                                                  # spp per render() call (main.cpp:272)
+
+CONFIGS = {
+    "C2": {"scene": "cornell_box", "width": 512, "height": 512, "spp": 64},
+    "C3": {"scene": "generated_scene", "width": 1920, "height": 1080, "spp": 1024},
+    "C4": {"scene": "generated_scene", "width": 3840, "height": 2160, "spp": 4096},
+    "C5": {"scene": "stress_100k", "width": 1920, "height": 1080, "spp": 4096},
+}
 
 
 def parse_args():
@@ -42,63 +61,220 @@ def parse_args():
     p.add_argument("--gpus", type=int, default=1)
     p.add_argument("--steps", type=int, default=3)
     p.add_argument("--warmup", type=int, default=1)
-    p.add_argument("--scene", default=str(ROOT / "scenes" / "generated_scene.scene.json"))
-    p.add_argument("--width", type=int, default=1920)
-    p.add_argument("--height", type=int, default=1080)
-    p.add_argument("--spp", type=int, default=1024)
-    p.add_argument("--chunk", type=int, default=8)
+    p.add_argument("--config", choices=sorted(CONFIGS), default="C3")
+    p.add_argument("--spp", type=int, default=0, help="override the config's spp (multiple of 8)")
+    p.add_argument("--scaling", choices=["weak", "strong"], default="strong",
+                   help="strong: the same workload for every N (default); weak: the image grows by sqrt(N) per axis")
+    p.add_argument("--band-rows", type=int, default=8, help="rows per band of the multi-GPU partition")
+    p.add_argument("--secondary", type=int, default=1, help="N=1: add the C2 record; N>1: add a weak-scaling record")
     p.add_argument("--cpu-baseline", type=int, default=1, help="time the oracle on a bounded sample (rank 0, N=1)")
-    p.add_argument("--scaling", choices=["weak", "strong"], default="weak",
-                   help="weak: per-GPU work fixed (image grows with N); strong: the same 1080p image for every N")
-    p.add_argument("--cpu-threads", type=int, default=0)
-    p.add_argument("--cpu-spp", type=int, default=192)
+    p.add_argument("--cpu-seconds", type=float, default=15.0, help="target length of the CPU baseline run")
+    p.add_argument("--cpu-threads", type=int, default=0, help="0 = every core this process may use")
     return p.parse_args()
 
 
-def algorithmic_bytes(stats: dict, pixels: int, launches: int) -> float:
+def scene_path(name: str) -> str:
+    if name == "stress_100k":
+        p = pathlib.Path(tempfile.gettempdir()) / "pt_stress_100k.json"
+        if not p.exists():
+            import importlib.util
+            spec = importlib.util.spec_from_file_location("mss", ROOT / "tools" / "make_stress_scene.py")
+            mod = importlib.util.module_from_spec(spec)
+            spec.loader.exec_module(mod)
+            mod.write_scene(p, grid=317, skybox=str(ROOT / "scenes" / "skybox.hdr"))
+        return str(p)
+    return str(ROOT / "scenes" / f"{name}.scene.json")
+
+
+def workload_name(cfg: dict, W: int, H: int, spp: int) -> str:
+    return f"{cfg['scene']} {W}x{H} {spp}spp chunk{CHUNK}"
+
+
+def algorithmic_bytes(stats: dict) -> float:
     return (NODE_B * stats["node_tests"] + PRIM_B * stats["prim_tests"] + MAT_B * stats["hits"]
-            + SKY_B * stats["sky_lookups"] + PIXEL_STATE_B * pixels * launches)
+            + SKY_B * stats["sky_lookups"])
 
 
-def load_pmc_traffic(workload: str):
-    """Per-launch HBM bytes of the trace kernel from the committed rocprofv3 --pmc summary, and the
-    issue utilisation of the same launch over shader-active cycles (GRBM_GUI_ACTIVE summed over the
-    8 XCDs): VALU = wave64 VALU instructions x 2 cycles (CDNA4 SIMD-32 throughput,
-    MI355X_MICROARCH.md cycle table) over 1024 SIMDs; SALU = scalar instructions per CU-cycle (one
-    scalar unit per CU, shared by its 4 SIMDs)."""
+def load_profile(workload: str):
+    """Per-launch counters of the trace kernel from the newest committed rocprofv3 --pmc summary of
+    this workload (profiles/*pmc_traffic*.json): HBM bytes (FETCH_SIZE x2 + WRITE_SIZE, gfx950
+    correction), wave64 VALU and scalar instructions, shader-active cycles (GRBM_GUI_ACTIVE summed
+    over the 8 XCDs)."""
     for f in sorted((ROOT / "profiles").glob("*pmc_traffic*.json"), reverse=True):
         try:
             d = json.loads(f.read_text())
         except (OSError, ValueError):
             continue
         if d.get("workload") == workload and d.get("bytes_per_launch"):
-            c = d.get("counters", {})
-            util = {}
-            cyc = c.get("GRBM_GUI_ACTIVE", 0) / 8.0
-            if cyc and c.get("SQ_INSTS_VALU"):
-                util["valu_util"] = round(2.0 * c["SQ_INSTS_VALU"] / (1024.0 * cyc), 3)
-            if cyc and c.get("SQ_INSTS_SALU"):
-                util["salu_per_cu_cycle"] = round(c["SQ_INSTS_SALU"] / (256.0 * cyc), 3)
-            return float(d["bytes_per_launch"]), f.name, util
-    return None, None, {}
+            return d, f.name
+    return None, None
 
 
-def cpu_baseline(args, W, H):
-    """Oracle (plain-C restatement, pthreads) on a bounded sample of the same workload."""
+def cpu_info():
+    model = platform.processor() or ""
+    try:
+        for line in open("/proc/cpuinfo"):
+            if line.startswith("model name"):
+                model = line.split(":", 1)[1].strip()
+                break
+    except OSError:
+        pass
+    quota = None
+    try:
+        q, per = open("/sys/fs/cgroup/cpu.max").read().split()
+        if q != "max":
+            quota = float(q) / float(per)
+    except (OSError, ValueError):
+        pass
+    return model, quota
+
+
+def cpu_baseline(args, cfg, W, H):
+    """The oracle (plain-C restatement of the reference's trace(), -O3 timing build, pthreads with
+    dynamic row scheduling) on every core this process may use, over the full image at a reduced
+    spp chosen from a pilot run so the run lasts about --cpu-seconds."""
     from oracle import pyoracle as po
-    threads = args.cpu_threads or min(16, len(os.sched_getaffinity(0)))
-    stride = 1                     # the full 1080p frame, fewer samples per pixel (~10 s of CPU work)
-    sc = po.load_scene(args.scene, W, H)
-    r = po.OracleRenderer(sc, W, H, 0, stride, threads=threads)
-    spp = min(args.chunk, args.cpu_spp)
-    chunks = max(1, args.cpu_spp // spp)
+    affinity = len(os.sched_getaffinity(0))
+    model, quota = cpu_info()
+    threads = args.cpu_threads or affinity
+    sc = po.load_scene(scene_path(cfg["scene"]), W, H)
+    pilot = po.OracleRenderer(sc, W, H, 0, max(1, H // 64), threads=threads, fast=True)
     t0 = time.perf_counter()
-    r.render(sc.camera, spp, True, chunks=chunks)
+    pilot.render(sc.camera, CHUNK, True, chunks=1)
+    rate = pilot.rows * W * CHUNK / max(time.perf_counter() - t0, 1e-6)
+    chunks = max(1, min(cfg["spp"] // CHUNK, int(args.cpu_seconds * rate / (W * H * CHUNK))))
+    r = po.OracleRenderer(sc, W, H, threads=threads, fast=True)
+    t0 = time.perf_counter()
+    r.render(sc.camera, CHUNK, True, chunks=chunks)
     dt = time.perf_counter() - t0
-    samples = r.rows * W * spp * chunks
+    samples = W * H * CHUNK * chunks
     return {"value": round(samples / dt / 1e6, 3), "unit": "Msamples/s", "cores": threads, "kind": "port",
-            "sample": f"{W}x{H} rows 0::{stride} ({r.rows} rows) x {spp * chunks} spp = {samples} samples, "
-                      f"{dt:.1f} s on {threads} threads"}
+            "sample": f"{cfg['scene']} {W}x{H} x {CHUNK * chunks} spp (of {cfg['spp']}) = {samples} samples, "
+                      f"{dt:.1f} s on {threads} threads",
+            "cpu_model": model, "affinity_cpus": affinity, "cgroup_cpu_limit": quota,
+            "build": "oracle/liboracle_fast.so: gcc -O3 -march=x86-64-v3 -ffp-contract=off (bit-identical to the checker)"}
+
+
+class Run:
+    """One workload on this rank: context, camera, gather buffers."""
+
+    def __init__(self, cfg, W, H, spp, rank, n, local_rank, band_rows, dist_on):
+        import torch
+        import pathtracercuda_amd as pa
+        from pathtracercuda_amd.distributed import global_rows, max_rows
+
+        self.cfg, self.W, self.H, self.spp = cfg, W, H, spp
+        self.rank, self.n, self.dist_on = rank, n, dist_on
+        self.chunks = spp // CHUNK
+        assert self.chunks * CHUNK == spp, "spp must be a multiple of 8"
+        self.band_rows = band_rows if dist_on else 1
+        self.pt = pa.Pathtracer(W, H, device=local_rank, row_offset=rank if dist_on else 0,
+                                row_stride=n if dist_on else 1, band_rows=self.band_rows)
+        self.cam = self.pt.load_scene(scene_path(cfg["scene"]))
+        if dist_on:
+            dev = f"cuda:{local_rank}"
+            self.send = torch.zeros((max_rows(H, n, self.band_rows), W, 4), dtype=torch.float32, device=dev)
+            self.recv = [torch.zeros_like(self.send) for _ in range(n)] if rank == 0 else None
+            self.full = torch.empty((H, W, 4), dtype=torch.float32, device=dev) if rank == 0 else None
+            self.index = ([torch.tensor(global_rows(H, r, n, self.band_rows), dtype=torch.long, device=dev)
+                           for r in range(n)] if rank == 0 else None)
+
+    def instrument(self):
+        # one untimed 8-spp chunk with the non-speculative child-box kernel, whose node/primitive
+        # tests are the reference's, for the algorithmic byte count and the lane utilisation; the
+        # launch also records the tile costs, so every timed launch runs in cost order
+        self.pt.set_kernel_variant(20)
+        st = self.pt.render_instrumented(self.cam, CHUNK, 1, True)
+        self.pt.set_kernel_variant(0)
+        return st
+
+    def step(self):
+        ms = self.pt.render_raw(self.cam, CHUNK, self.chunks, True)
+        if self.dist_on:
+            from pathtracercuda_amd.distributed import gather_framebuffer
+            # RCCL framebuffer gather over xGMI + scatter of the bands on rank 0
+            self.pt.copy_accum_to_device(self.send.data_ptr(), self.send.numel() * 4)
+            gather_framebuffer(self.send, self.H, self.rank, self.n, recv=self.recv, full=self.full,
+                               band_rows=self.band_rows, index=self.index)
+        return ms
+
+    def close(self):
+        self.pt.close()
+
+
+def timed(run, steps, warmup, local_rank, dist_on):
+    import torch
+    import torch.distributed as dist
+
+    def barrier_sync():
+        torch.cuda.synchronize(local_rank)
+        if dist_on:
+            dist.barrier()
+
+    for _ in range(warmup):
+        run.step()
+    barrier_sync()
+    t0 = time.perf_counter()
+    kernel_ms = 0.0
+    for _ in range(steps):
+        kernel_ms += run.step()
+    barrier_sync()
+    elapsed = time.perf_counter() - t0
+    if dist_on:
+        t = torch.tensor([elapsed, kernel_ms], dtype=torch.float64, device=f"cuda:{local_rank}")
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed, kernel_ms = float(t[0]), float(t[1])
+    return elapsed, kernel_ms
+
+
+def lane_utilisation(st):
+    """SIMD efficiency of each phase of the instrumented launch: lane-level events / (64 x wave-level
+    executions).  An interior child-box visit counts two node tests per lane and one wave tick; the
+    root test of each segment counts one of each."""
+    def ratio(lanes, waves):
+        return round(lanes / (64.0 * waves), 3) if waves else None
+    visits = (st["node_tests"] + st["segments"]) / 2.0
+    return {"interior_walk": ratio(visits, st["wave_node_iters"]), "leaf_tests": ratio(st["prim_tests"], st["wave_prim_iters"]),
+            "hit_shading": ratio(st["hits"], st["wave_hits"]), "sky_shading": ratio(st["sky_lookups"], st["wave_sky"])}
+
+
+def record(cfg, run, elapsed, kernel_ms, steps, st, n, with_profile=True):
+    W, H, spp = run.W, run.H, run.spp
+    total_samples = W * H * spp * steps
+    avg_launch_s = kernel_ms / steps / 1e3
+    samples_launch = W * H * spp / n                              # per GPU
+    alg = algorithmic_bytes(st) / max(st["samples"], 1) * samples_launch + PIXEL_STATE_B * W * H / n
+    workload = workload_name(cfg, W, H, spp)
+    prof, src = load_profile(workload) if with_profile else (None, None)
+    if prof is None and with_profile:      # e.g. weak scaling: the same scene's base workload, per sample
+        prof, src = load_profile(workload_name(cfg, cfg["width"], cfg["height"], cfg["spp"]))
+    scale = 1.0
+    if prof:                               # the profile is one whole-image launch on one GPU
+        dims, pspp = prof["workload"].split()[1], prof["workload"].split()[2]
+        pw, ph = (int(x) for x in dims.split("x"))
+        scale = samples_launch / (pw * ph * int(pspp[:-3]))
+    roof = {"bound": "valu_issue", "achieved": None, "peak": round(VALU_PEAK_G, 1), "unit": "G wave64-VALU-instr/s",
+            "frac": None, "traffic": None, "kernel": "trace_kernel", "avg_launch_ms": round(avg_launch_s * 1e3, 3),
+            "lds_l2_effective_GBs": round(alg / avg_launch_s / 1e9, 1),
+            "bytes_per_sample": round(alg / samples_launch, 1),
+            "lane_utilisation": lane_utilisation(st)}
+    if prof:
+        c = prof["counters"]
+        valu = c["SQ_INSTS_VALU"] * scale
+        cyc = c.get("GRBM_GUI_ACTIVE", 0) / 8.0
+        roof.update({
+            "achieved": round(valu / avg_launch_s / 1e9, 1),
+            "frac": round(valu / avg_launch_s / 1e9 / VALU_PEAK_G, 4),
+            "traffic": round(prof["bytes_per_launch"] * scale),
+            "valu_instr_per_launch": round(valu),
+            "valu_busy_measured": round(2.0 * c["SQ_INSTS_VALU"] / (SIMDS * cyc), 3) if cyc else None,
+            "salu_per_cu_cycle": round(c["SQ_INSTS_SALU"] / (256.0 * cyc), 3) if cyc and c.get("SQ_INSTS_SALU") else None,
+            "hbm_GBs_measured": round(prof["bytes_per_launch"] * scale / avg_launch_s / 1e9, 1),
+            "hbm_frac_measured": round(prof["bytes_per_launch"] * scale / avg_launch_s / 1e9 / HBM_PEAK_GBS, 5),
+            "profile": src + ("" if scale == 1.0 else f" (per-launch counts x {scale:.4f}: this GPU's share)"),
+        })
+    return {"value": round(total_samples / elapsed / 1e6, 3), "unit": "Msamples/s", "ms_per_step": round(elapsed * 1e3 / steps, 3),
+            "workload": workload, "roofline": roof}
 
 
 def main():
@@ -110,115 +286,79 @@ def main():
         print(f"bench.py: --gpus {args.gpus} needs one process per GPU (torch.distributed.run "
               f"--nproc-per-node {args.gpus}); running on 1 GPU", file=sys.stderr)
     n = max(1, world)
-    W, H, spp, chunk = args.width, args.height, args.spp, args.chunk
+    cfg = CONFIGS[args.config]
+    W, H, spp = cfg["width"], cfg["height"], args.spp or cfg["spp"]
     if args.scaling == "weak" and n > 1:
-        # weak scaling: every GPU keeps one 1080p frame's worth of pixels; the image grows by
-        # sqrt(N) per axis (N = 4 is 3840x2160, the C4 resolution), rows interleaved over ranks
         W = int(round(W * math.sqrt(n) / 8.0)) * 8
         H = int(round(H * math.sqrt(n) / 8.0)) * 8
-    chunks = spp // chunk
-    assert chunks * chunk == spp, "spp must be a multiple of --chunk"
 
     import torch
     import torch.distributed as dist
-    import pathtracercuda_amd as pa
 
     dist_on = world > 1
     if dist_on:
         torch.cuda.set_device(local_rank)
         dist.init_process_group("nccl", device_id=torch.device("cuda", local_rank))
-    device = local_rank
-    pt = pa.Pathtracer(W, H, device=device, row_offset=rank if dist_on else 0, row_stride=n if dist_on else 1)
-    cam = pt.load_scene(args.scene)
-    rows_max = (H + n - 1) // n
-    if dist_on:
-        send = torch.zeros((rows_max, W, 4), dtype=torch.float32, device=f"cuda:{local_rank}")
-        recv = [torch.zeros_like(send) for _ in range(n)] if rank == 0 else None
-        full = torch.empty((H, W, 4), dtype=torch.float32, device=f"cuda:{local_rank}") if rank == 0 else None
 
-    from pathtracercuda_amd.distributed import gather_framebuffer
+    def stats_all(st):
+        if not dist_on:
+            return st
+        keys = ("node_tests", "prim_tests", "hits", "sky_lookups", "samples", "segments", "wave_node_iters",
+                "wave_prim_iters", "wave_hits", "wave_sky")
+        t = torch.tensor([st[k] for k in keys], dtype=torch.float64, device=f"cuda:{local_rank}")
+        dist.all_reduce(t)
+        return dict(zip(keys, [float(x) for x in t]))
 
-    def gather():
-        # RCCL framebuffer gather over xGMI + unpermute of the interleaved rows on rank 0
-        pt.copy_accum_to_device(send.data_ptr(), send.numel() * 4)
-        gather_framebuffer(send, H, rank, n, recv=recv, full=full)
-
-    def step():
-        ms = pt.render_raw(cam, chunk, chunks, True)
-        if dist_on:
-            gather()
-        return ms
-
-    def barrier_sync():
-        torch.cuda.synchronize(device)
-        if dist_on:
-            dist.barrier()
-
-    # instrumented run (not timed): algorithmic byte count of this workload, 1 chunk.  Counted
-    # with the non-speculative child-box kernel, whose node/primitive tests are the reference's
-    # (the speculative variant adds node tests of its own); then back to automatic selection.
-    pt.set_kernel_variant(20)
-    stats = pt.render_instrumented(cam, chunk, 1, True)
-    pt.set_kernel_variant(0)    # (that launch also recorded the tile costs: every timed launch is cost-ordered)
-    samples_per_chunk = stats["samples"]
-    for _ in range(args.warmup):
-        step()
-    barrier_sync()
-    t0 = time.perf_counter()
-    kernel_ms = 0.0
-    for _ in range(args.steps):
-        kernel_ms += step()
-    barrier_sync()
-    elapsed = time.perf_counter() - t0
-    if dist_on:
-        t = torch.tensor([elapsed, kernel_ms], dtype=torch.float64, device=f"cuda:{local_rank}")
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        elapsed, kernel_ms = float(t[0]), float(t[1])
-        st = torch.tensor([stats[k] for k in ("node_tests", "prim_tests", "hits", "sky_lookups", "samples")],
-                          dtype=torch.float64, device=f"cuda:{local_rank}")
-        dist.all_reduce(st)
-        stats = dict(zip(("node_tests", "prim_tests", "hits", "sky_lookups", "samples"), [float(x) for x in st]))
-        samples_per_chunk = stats["samples"]
-
-    total_samples = W * H * spp * args.steps
-    ms_per_step = elapsed * 1e3 / args.steps
-    value = total_samples / elapsed / 1e6
-    # roofline of the trace kernel: algorithmic bytes of one launch (= one step per GPU)
-    launch_bytes = algorithmic_bytes(stats, 0, 0) * chunks + PIXEL_STATE_B * W * H   # whole image per step
-    per_gpu_bytes = launch_bytes / n
-    avg_launch_s = kernel_ms / args.steps / 1e3
-    achieved = per_gpu_bytes / avg_launch_s / 1e9
-    workload = f"generated_scene {W}x{H} {spp}spp chunk{chunk}"
-    traffic, traffic_src, util = load_pmc_traffic(workload)
+    run = Run(cfg, W, H, spp, rank, n, local_rank, args.band_rows, dist_on)
+    st = stats_all(run.instrument())
+    elapsed, kernel_ms = timed(run, args.steps, args.warmup, local_rank, dist_on)
+    main_rec = record(cfg, run, elapsed, kernel_ms, args.steps, st, n)
+    run.close()
+    part = (f"{args.band_rows}-row bands interleaved x{n}, RCCL gather" if dist_on else "1 GPU")
     out = {
-        "metric": "Msamples/sec + achieved HBM GB/s, 1080p 1024spp, 1/2/4/8 MI355X",
-        "value": round(value, 3),
+        "metric": METRIC,
+        "value": main_rec["value"],
         "unit": "Msamples/s",
         "n_gpus": n,
         "steps": args.steps,
         "warmup": args.warmup,
-        "ms_per_step": round(ms_per_step, 3),
+        "ms_per_step": main_rec["ms_per_step"],
         "higher_is_better": True,
         "scaling": args.scaling,
         "vs_baseline": None,
         "dtype": "f32",
-        "data": "synthetic sky (scenes/skybox.hdr), reference scene generated_scene.json",
-        "config": {"workload": workload, "scene": "generated_scene.json (484 quadrics)", "width": W, "height": H,
-                   "spp": spp, "render_calls_per_step": chunks, "parallelism": f"rows interleaved x{n}, RCCL gather",
+        "data": "synthetic sky (scenes/skybox.hdr); reference scene files (scenes/)",
+        "config": {"workload": main_rec["workload"], "label": args.config, "scene": cfg["scene"], "width": W,
+                   "height": H, "spp": spp, "render_calls_per_step": spp // CHUNK, "parallelism": part,
                    "per_gpu_pixels": (W * H + n - 1) // n},
-        "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                     "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic,
-                     "kernel": "trace_kernel", "avg_launch_ms": round(avg_launch_s * 1e3, 3),
-                     "bytes_per_sample": round(launch_bytes / (W * H * spp), 1),
-                     "traffic_source": traffic_src,
-                     # the algorithmic bytes are served from LDS and L2 (traffic = HBM bytes measured);
-                     # the kernel is issue/latency-bound: VALU and scalar-unit use from the same profile
-                     "hbm_frac_measured": (round(traffic / avg_launch_s / 1e9 / HBM_PEAK_GBS, 5) if traffic else None),
-                     **util},
+        "roofline": main_rec["roofline"],
         "cpu_baseline": None,
     }
+    if args.secondary:
+        if n == 1:
+            c2 = CONFIGS["C2"]
+            r2 = Run(c2, c2["width"], c2["height"], c2["spp"], 0, 1, local_rank, 1, False)
+            st2 = r2.instrument()
+            e2, k2 = timed(r2, max(args.steps, 5), args.warmup, local_rank, False)
+            rec2 = record(c2, r2, e2, k2, max(args.steps, 5), st2, 1)
+            r2.close()
+            rec2["label"] = "C2"
+            if rank == 0 and args.cpu_baseline:
+                rec2["cpu_baseline"] = cpu_baseline(args, c2, c2["width"], c2["height"])
+            out["secondary"] = [rec2]
+        elif args.scaling == "strong":
+            Ww = int(round(cfg["width"] * math.sqrt(n) / 8.0)) * 8
+            Hw = int(round(cfg["height"] * math.sqrt(n) / 8.0)) * 8
+            rw = Run(cfg, Ww, Hw, spp, rank, n, local_rank, args.band_rows, dist_on)
+            stw = stats_all(rw.instrument())
+            ew, kw = timed(rw, min(args.steps, 3), 1, local_rank, dist_on)
+            recw = record(cfg, rw, ew, kw, min(args.steps, 3), stw, n)
+            rw.close()
+            recw["label"] = f"{args.config} weak scaling (image {Ww}x{Hw}: one {cfg['width']}x{cfg['height']} frame per GPU)"
+            recw["scaling"] = "weak"
+            out["secondary"] = [recw]
     if rank == 0 and n == 1 and args.cpu_baseline:
-        out["cpu_baseline"] = cpu_baseline(args, W, H)
+        out["cpu_baseline"] = cpu_baseline(args, cfg, W, H)
     if rank == 0:
         print(json.dumps(out), flush=True)
     if dist_on:

@@ -10,8 +10,9 @@
 //   Pathtracer               src/pathtracer/Pathtracer.h:12-68
 //   Params                   src/Params.h:4-13
 //   loadScene                src/SceneLoader.h:9, SceneLoader.cpp:124-348
-// Differences (all additive): a Pathtracer can own a row tile of a larger image (multi-GPU), a
-// device index can be chosen, and renderChunks() runs several render() calls in one launch.
+// Differences (all additive): a Pathtracer can own a row-band tile of a larger image or span
+// several GPUs of the process (RCCL gather), a device index can be chosen, and renderChunks()
+// runs several render() calls in one launch.
 // All host arithmetic follows the reference operation for operation (built with
 // -ffp-contract=off) so BVHs, transforms and cameras are bit-identical to the reference's.
 #pragma once
@@ -176,6 +177,17 @@ public:
     explicit Pathtracer(uint32_t width, uint32_t height, unsigned int openglPixelBuffer = 0);
     // Row tile of a width x height image on `device`: rows y = rowOffset + k * rowStride.
     Pathtracer(uint32_t width, uint32_t height, int device, uint32_t rowOffset, uint32_t rowStride);
+    // Band tile on `device`: the bands of bandRows rows b = bandOffset + k * bandStride
+    // (pt_create_banded); bandRows = 1 is the row tile above.
+    struct Tile {
+        int device;
+        uint32_t bandRows, bandOffset, bandStride;
+    };
+    Pathtracer(uint32_t width, uint32_t height, const Tile& tile);
+    // The whole image on several GPUs of this process (the CLI's -gpus N): device i renders the row
+    // bands i, i + N, ... and getHDRImageData / getImageData return the full image, gathered on
+    // devices[0] over RCCL (pt_group_*).  Bit-identical to a single-device render.
+    Pathtracer(uint32_t width, uint32_t height, const std::vector<int>& devices, uint32_t bandRows = 8);
     Pathtracer(const Pathtracer&) = delete;
     Pathtracer(const Pathtracer&&) = delete;
     Pathtracer& operator=(const Pathtracer&) = delete;
@@ -196,9 +208,12 @@ public:
     // additions
     uint32_t width() const { return m_width; }
     uint32_t height() const { return m_height; }
-    uint32_t localRows() const;
+    uint32_t localRows() const;     // rows of the image data this object returns
     uint32_t accumulatedFrames() const { return m_accumulatedFrames; }
-    pt_context* context() const { return m_ctx; }
+    pt_context* context() const { return m_ctx; }    // device context (devices[0]'s for a group)
+    pt_group* group() const { return m_group; }      // null unless multi-device
+    int deviceCount() const { return m_group ? pt_group_size(m_group) : 1; }
+    float lastGatherMs() const { return m_gatherMs; }
     const BVH& bvh() const { return m_bvh; }
 
 private:
@@ -213,7 +228,10 @@ private:
     std::vector<float> m_cpuAccumBuffer;
     std::vector<char> m_cpuResultBuffer;
     pt_context* m_ctx = nullptr;
+    pt_group* m_group = nullptr;
+    float m_gatherMs = 0.0f;
     BVH m_bvh;
+    void allocHostBuffers();
     void check(int rc, const char* what) const;
 };
 

@@ -108,6 +108,17 @@ PT_API int pt_device_count(int *count);
  * seeds and camera coordinates always use global pixel coordinates. */
 PT_API int pt_create(int device, uint32_t width, uint32_t height, uint32_t row_offset, uint32_t row_stride,
                      pt_context **out);
+
+/* Same, tiling the image in bands of band_rows rows (a power of two, 1..256): the context covers
+ * the bands b = band_offset + k * band_stride, i.e. global row
+ *     y(ly) = (band_offset + (ly / band_rows) * band_stride) * band_rows + ly % band_rows
+ * for local row ly.  band_rows = 1 is pt_create's row interleave; band_rows = 8 (the multi-GPU
+ * default) keeps each 8x8 tile of a context a spatially coherent 8x8 tile of the image. */
+PT_API int pt_create_banded(int device, uint32_t width, uint32_t height, uint32_t band_rows, uint32_t band_offset,
+                            uint32_t band_stride, pt_context **out);
+
+/* Number of local rows of such a context (0 if it owns no band or the arguments are invalid). */
+PT_API uint32_t pt_band_rows(uint32_t height, uint32_t band_rows, uint32_t band_offset, uint32_t band_stride);
 PT_API void pt_destroy(pt_context *ctx);
 
 /* Pathtracer::setScene upload half (Pathtracer.cpp:137-159): nodes and primitives as produced by
@@ -128,8 +139,11 @@ PT_API int pt_set_skybox(pt_context *ctx, uint32_t handle);
  * successive reference render(camera, spp, ignore) calls where the first call uses
  * ignore = ignore_history and the others ignore = false (the headless loop, main.cpp:275-279).
  * Synchronous.  gpu_ms (optional) receives the kernel time measured with hipEvents on the
- * context's stream.  No launch (and no error) when no scene is set or spp == 0, as in the
- * reference (Pathtracer.cpp:174). */
+ * context's stream (it includes the cost pre-pass below).  No launch (and no error) when no scene
+ * is set or spp == 0, as in the reference (Pathtracer.cpp:174).
+ * Tiles are dispatched most expensive first.  When no cost order is known yet for the scene and
+ * camera and spp * chunks >= 16, a 2-spp pre-pass that writes nothing back measures the tile
+ * costs first; results never depend on the order. */
 PT_API int pt_render(pt_context *ctx, const pt_camera *camera, uint32_t spp, uint32_t chunks, int ignore_history,
                      float *gpu_ms);
 
@@ -158,9 +172,10 @@ PT_API int pt_write_rng(pt_context *ctx, const uint32_t *src);
 
 PT_API uint32_t pt_local_rows(const pt_context *ctx);
 
-/* Tuning knob for A/B measurements: 0 = automatic (default); 1..45 select a trace-kernel variant
- * (workgroup size, BVH/primitives staged in LDS or read through the caches, traversal loop shape,
- * occupancy target).  All variants produce bit-identical results. */
+/* Tuning knob for A/B measurements: 0 = automatic (default); otherwise one of the shipped
+ * trace-kernel variants 1, 4, 6, 20, 40, 41, 46 (traversal loop shape, BVH staged in LDS or read
+ * through the caches, occupancy target; see pt_kernels.hip).  All variants produce bit-identical
+ * results.  Other numbers return PT_ERR_ARG. */
 PT_API int pt_set_kernel_variant(pt_context *ctx, int variant);
 
 /* Tile dispatch order: 0 = by the measured cost of each 8x8 tile, most expensive first (default:
@@ -169,6 +184,37 @@ PT_API int pt_set_kernel_variant(pt_context *ctx, int variant);
  * only the launch tail changes. */
 PT_API int pt_set_schedule(pt_context *ctx, int mode);
 PT_API const char *pt_last_error(const pt_context *ctx);
+
+/* ---- Multi-device group (one process, one context per GPU, RCCL over xGMI) -------------------
+ * Replaces the reference's hard-coded single device (Pathtracer.cpp:40: cudaSetDevice(0)) behind
+ * the same Pathtracer interface: device i renders the row bands b = i, i + N, ... of the image
+ * (pt_create_banded with band_offset = i, band_stride = N), and pt_group_gather assembles the
+ * accumulation buffer on devices[0] with one grouped ncclSend/ncclRecv (communicators from
+ * ncclCommInitAll) plus an unpermute kernel.  Seeds use global pixel indices, so the assembled
+ * image is bit-identical to a single-device render.  Devices must be distinct. */
+typedef struct pt_group pt_group;
+
+PT_API int pt_group_create(int ndev, const int *devices, uint32_t width, uint32_t height, uint32_t band_rows,
+                           pt_group **out);
+PT_API void pt_group_destroy(pt_group *g);
+PT_API int pt_group_size(const pt_group *g);
+/* The context of device index i (for per-device calls such as pt_set_kernel_variant). */
+PT_API pt_context *pt_group_context(pt_group *g, int index);
+PT_API int pt_group_set_scene(pt_group *g, const pt_bvh_node *nodes, uint32_t node_count, const pt_hittable *prims,
+                              uint32_t prim_count);
+PT_API int pt_group_set_texture(pt_group *g, uint32_t handle, const float *rgba, uint32_t width, uint32_t height);
+PT_API int pt_group_set_skybox(pt_group *g, uint32_t handle);
+/* pt_render on every device concurrently (one host thread each); gpu_ms = the slowest device. */
+PT_API int pt_group_render(pt_group *g, const pt_camera *camera, uint32_t spp, uint32_t chunks, int ignore_history,
+                           float *gpu_ms);
+/* RCCL gather of every device's accumulation rows to devices[0] + unpermute into the full image;
+ * host_ms (optional) = wall time of the gather. */
+PT_API int pt_group_gather(pt_group *g, float *host_ms);
+/* Full-image raw accumulation (height x width float4, y-up) / tonemap (RGBA8), gathering first if
+ * the image changed since the last gather. */
+PT_API int pt_group_read_accum(pt_group *g, float *dst);
+PT_API int pt_group_tonemap(pt_group *g, uint32_t frames, uint8_t *dst);
+PT_API const char *pt_group_last_error(const pt_group *g);
 
 #ifdef __cplusplus
 }

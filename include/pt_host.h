@@ -57,6 +57,15 @@ PT_API float pth_radians(float degrees);
 /* Pathtracer on `device`, covering rows y = row_offset + k * row_stride. */
 PT_API int pth_renderer_create(uint32_t width, uint32_t height, int device, uint32_t row_offset, uint32_t row_stride,
                                pth_renderer **out);
+/* Pathtracer on `device`, covering the row bands b = band_offset + k * band_stride of band_rows
+ * rows each (pt_create_banded). */
+PT_API int pth_renderer_create_banded(uint32_t width, uint32_t height, int device, uint32_t band_rows,
+                                      uint32_t band_offset, uint32_t band_stride, pth_renderer **out);
+/* Pathtracer over several GPUs of this process (pt_group_*): the image data calls return the full
+ * image, gathered on devices[0] over RCCL; pth_renderer_gather_ms = wall time of the last gather. */
+PT_API int pth_renderer_create_group(uint32_t width, uint32_t height, int ndev, const int *devices, uint32_t band_rows,
+                                     pth_renderer **out);
+PT_API float pth_renderer_gather_ms(const pth_renderer *r);
 PT_API void pth_renderer_destroy(pth_renderer *r);
 /* loadScene(pathtracer, params) for a scene file; fills the camera (aspect = width / height). */
 PT_API int pth_renderer_load_scene(pth_renderer *r, const char *path, pt_camera *camera);
@@ -68,7 +77,8 @@ PT_API uint32_t pth_renderer_local_rows(const pth_renderer *r);
 /* getHDRImageData / getImageData: borrowed pointers, valid until the next call */
 PT_API const float *pth_renderer_hdr(pth_renderer *r);
 PT_API const uint8_t *pth_renderer_image(pth_renderer *r);
-PT_API pt_context *pth_renderer_context(pth_renderer *r);
+PT_API pt_context *pth_renderer_context(pth_renderer *r);   /* devices[0]'s context for a group */
+PT_API pt_group *pth_renderer_group(pth_renderer *r);       /* null unless multi-device */
 
 /* Output files (main.cpp:180-199 semantics: rows flipped vertically when flip != 0). */
 PT_API int pth_write_png(const char *path, uint32_t width, uint32_t height, const uint8_t *rgba, int flip);

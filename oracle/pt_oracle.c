@@ -1277,15 +1277,38 @@ static v3 get_color(const or_scene *s, ray_t ray, xorwow_t *rng, or_stats *st, i
 
 /* ------------------------------------------------------------------------------------------ */
 /* Kernels: initRandState (initRandState.cu:4-17), traceKernel (trace.cu:158-199), tonemap     */
-/* (tonemap.cu:4-27).  Pixels are addressed by global (x, y); a "view" selects rows             */
-/* y = row_offset + k * row_stride so multi-GPU row tiles can be reproduced.                     */
+/* (tonemap.cu:4-27).  Pixels are addressed by global (x, y); a "view" selects the row bands     */
+/* b = band_offset + k * band_stride of band_rows rows each (band_rows = 1: rows                   */
+/* y = offset + k * stride) so multi-GPU tiles can be reproduced.  Written out independently of   */
+/* the kernel's global_row (pt_kernels.hip): the band of local row k is k / band_rows.            */
 /* ------------------------------------------------------------------------------------------ */
-OR_EXPORT void or_init_rand_state(uint32_t width, uint32_t height, uint32_t row_offset, uint32_t row_stride,
-                                  xorwow_t *states)
+static uint32_t view_rows(uint32_t height, uint32_t band_rows, uint32_t offset, uint32_t stride)
 {
-    uint32_t rows = row_offset < height ? (height - row_offset + row_stride - 1) / row_stride : 0;
+    uint32_t rows = 0;
+    for (uint32_t b = offset; (uint64_t)b * band_rows < height; b += stride) {
+        uint32_t end = (b + 1) * band_rows < height ? (b + 1) * band_rows : height;
+        rows += end - b * band_rows;
+    }
+    return rows;
+}
+
+static uint32_t view_row(uint32_t k, uint32_t band_rows, uint32_t offset, uint32_t stride)
+{
+    uint32_t band = offset + (k / band_rows) * stride;
+    return band * band_rows + k % band_rows;
+}
+
+OR_EXPORT uint32_t or_view_rows(uint32_t height, uint32_t band_rows, uint32_t offset, uint32_t stride)
+{
+    return view_rows(height, band_rows, offset, stride);
+}
+
+OR_EXPORT void or_init_rand_state(uint32_t width, uint32_t height, uint32_t band_rows, uint32_t row_offset,
+                                  uint32_t row_stride, xorwow_t *states)
+{
+    uint32_t rows = view_rows(height, band_rows, row_offset, row_stride);
     for (uint32_t k = 0; k < rows; ++k) {
-        uint32_t y = row_offset + k * row_stride;
+        uint32_t y = view_row(k, band_rows, row_offset, row_stride);
         for (uint32_t x = 0; x < width; ++x) {
             uint32_t idx = x + y * width;
             or_xorwow_init((uint64_t)(uint32_t)(1984u + idx), &states[(size_t)k * width + x]);
@@ -1298,8 +1321,9 @@ typedef struct {
     const or_camera *cam;
     float *accum;
     xorwow_t *rng;
-    uint32_t width, height, row_offset, row_stride, rows, spp, chunks, ignoreFirst;
+    uint32_t width, height, band_rows, row_offset, row_stride, rows, spp, chunks, ignoreFirst;
     uint32_t nthreads, tid, collect;
+    uint32_t *next_row;   /* shared cursor: rows are handed out dynamically (any order gives the same bits) */
     or_stats stats;
     int err;
 } render_job;
@@ -1307,8 +1331,10 @@ typedef struct {
 static void render_rows(render_job *j)
 {
     const or_camera *cam = j->cam;
-    for (uint32_t k = j->tid; k < j->rows; k += j->nthreads) {
-        uint32_t y = j->row_offset + k * j->row_stride;
+    for (;;) {
+        uint32_t k = __atomic_fetch_add(j->next_row, 1u, __ATOMIC_RELAXED);
+        if (k >= j->rows) break;
+        uint32_t y = view_row(k, j->band_rows, j->row_offset, j->row_stride);
         for (uint32_t x = 0; x < j->width; ++x) {
             size_t li = (size_t)k * j->width + x;
             xorwow_t st = j->rng[li];
@@ -1341,21 +1367,24 @@ static void *render_thread(void *p) { render_rows((render_job *)p); return NULL;
  * success, -1 if a traversal stack would overflow (undefined behaviour in the reference). */
 OR_EXPORT int or_render(const or_hittable *prims, uint32_t primCount, const or_bvh_node *nodes, uint32_t nodeCount,
                         const or_camera *cam, uint32_t skyboxHandle, const or_texture *textures, uint32_t textureCount,
-                        uint32_t width, uint32_t height, uint32_t row_offset, uint32_t row_stride, float *accum,
+                        uint32_t width, uint32_t height, uint32_t band_rows, uint32_t row_offset, uint32_t row_stride,
+                        float *accum,
                         xorwow_t *rng, uint32_t spp, uint32_t chunks, int ignore_first, int nthreads, uint64_t *stats_out)
 {
     or_scene s = { prims, primCount, nodes, nodeCount, skyboxHandle, textures, textureCount };
-    uint32_t rows = row_offset < height ? (height - row_offset + row_stride - 1) / row_stride : 0;
+    uint32_t rows = view_rows(height, band_rows, row_offset, row_stride);
     if (nodeCount < 1 || primCount < 1 || spp == 0) return 0; /* Pathtracer.cpp:174: no launch */
     if (nthreads < 1) nthreads = 1;
+    uint32_t next_row = 0;
     render_job *jobs = (render_job *)calloc((size_t)nthreads, sizeof(render_job));
     pthread_t *th = (pthread_t *)calloc((size_t)nthreads, sizeof(pthread_t));
     for (int t = 0; t < nthreads; ++t) {
         render_job *j = &jobs[t];
         j->scene = &s; j->cam = cam; j->accum = accum; j->rng = rng;
-        j->width = width; j->height = height; j->row_offset = row_offset; j->row_stride = row_stride; j->rows = rows;
+        j->width = width; j->height = height; j->band_rows = band_rows; j->row_offset = row_offset; j->row_stride = row_stride; j->rows = rows;
         j->spp = spp; j->chunks = chunks; j->ignoreFirst = (uint32_t)(ignore_first != 0);
         j->nthreads = (uint32_t)nthreads; j->tid = (uint32_t)t; j->collect = stats_out != NULL;
+        j->next_row = &next_row;
         if (nthreads > 1) pthread_create(&th[t], NULL, render_thread, j);
         else render_rows(j);
     }

@@ -23,6 +23,7 @@ import numpy as np
 
 HERE = pathlib.Path(__file__).resolve().parent
 LIB_PATH = HERE / "liboracle.so"
+FAST_LIB_PATH = HERE / "liboracle_fast.so"      # -O3 build of the same source (bench.py cpu_baseline)
 
 SHAPES = ["SPHERE", "CYLINDER", "DISK", "CONE", "PARABOLOID", "QUAD", "CUBE"]
 MATERIALS = ["LAMBERT", "GGX", "LAMBERT_GGX"]
@@ -62,14 +63,26 @@ class Xorwow(C.Structure):
 
 
 _lib = None
+_fast = None
 
 
-def lib() -> C.CDLL:
-    global _lib
+def lib(fast: bool = False) -> C.CDLL:
+    global _lib, _fast
+    if fast:
+        if _fast is None:
+            if not FAST_LIB_PATH.exists():
+                raise RuntimeError(f"{FAST_LIB_PATH} missing: run `make -C oracle`")
+            _fast = _bind(C.CDLL(str(FAST_LIB_PATH)))
+        return _fast
     if _lib is None:
         if not LIB_PATH.exists():
             raise RuntimeError(f"{LIB_PATH} missing: run `make -C oracle` (or __graft_entry__.build())")
-        L = C.CDLL(str(LIB_PATH))
+        _lib = _bind(C.CDLL(str(LIB_PATH)))
+    return _lib
+
+
+def _bind(L: C.CDLL) -> C.CDLL:
+    if True:   # (indentation kept from the single-library loader)
         f = C.c_float
         P = C.POINTER
         L.or_radians.restype = f
@@ -82,10 +95,12 @@ def lib() -> C.CDLL:
         L.or_camera_translate.argtypes = [P(Camera), f, f, f]
         L.or_bvh_build.restype = C.c_uint32
         L.or_bvh_build.argtypes = [C.c_size_t, P(CpuHittable), C.c_uint32, P(BVHNode)]
-        L.or_init_rand_state.argtypes = [C.c_uint32] * 4 + [P(Xorwow)]
+        L.or_init_rand_state.argtypes = [C.c_uint32] * 5 + [P(Xorwow)]
+        L.or_view_rows.restype = C.c_uint32
+        L.or_view_rows.argtypes = [C.c_uint32] * 4
         L.or_render.restype = C.c_int
         L.or_render.argtypes = [P(Hittable), C.c_uint32, P(BVHNode), C.c_uint32, P(Camera), C.c_uint32, P(Texture),
-                                C.c_uint32, C.c_uint32, C.c_uint32, C.c_uint32, C.c_uint32, P(f), P(Xorwow),
+                                C.c_uint32, C.c_uint32, C.c_uint32, C.c_uint32, C.c_uint32, C.c_uint32, P(f), P(Xorwow),
                                 C.c_uint32, C.c_uint32, C.c_int, C.c_int, P(C.c_uint64)]
         L.or_tonemap.argtypes = [P(f), C.c_size_t, C.c_uint32, P(C.c_uint8)]
         L.or_hdr_normalize.argtypes = [P(f), C.c_size_t, C.c_uint32, P(f)]
@@ -103,8 +118,7 @@ def lib() -> C.CDLL:
         L.or_tex2d.argtypes = [P(Texture), f, f, P(f)]
         L.or_sizeof.restype = C.c_uint32
         L.or_sizeof.argtypes = [C.c_int]
-        _lib = L
-    return _lib
+    return L
 
 
 def fptr(a: np.ndarray):
@@ -331,34 +345,36 @@ def load_scene(path: os.PathLike, width: int, height: int) -> OracleScene:
     return sc
 
 
-def rows_of(height: int, row_offset: int, row_stride: int) -> int:
-    return (height - row_offset + row_stride - 1) // row_stride if row_offset < height else 0
+def rows_of(height: int, row_offset: int, row_stride: int, band_rows: int = 1) -> int:
+    return int(lib().or_view_rows(height, band_rows, row_offset, row_stride))
 
 
 class OracleRenderer:
     """Per-pixel state of the reference Pathtracer (accum buffer, curandState, frame counter)
-    restricted to rows y = row_offset + k * row_stride."""
+    restricted to the row bands b = row_offset + k * row_stride of band_rows rows (band_rows = 1:
+    rows y = row_offset + k * row_stride)."""
 
     def __init__(self, scene: OracleScene, width: int, height: int, row_offset: int = 0, row_stride: int = 1,
-                 threads: Optional[int] = None) -> None:
+                 threads: Optional[int] = None, band_rows: int = 1, fast: bool = False) -> None:
         self.scene = scene
         self.width, self.height = width, height
-        self.row_offset, self.row_stride = row_offset, row_stride
-        self.rows = rows_of(height, row_offset, row_stride)
+        self.row_offset, self.row_stride, self.band_rows = row_offset, row_stride, band_rows
+        self.rows = rows_of(height, row_offset, row_stride, band_rows)
         self.accum = np.zeros((self.rows, width, 4), dtype=np.float32)
-        self.rng = (Xorwow * (self.rows * width))()
-        lib().or_init_rand_state(width, height, row_offset, row_stride, self.rng)
+        self.rng = (Xorwow * max(1, self.rows * width))()
+        lib().or_init_rand_state(width, height, band_rows, row_offset, row_stride, self.rng)
         self.frames = 0
         self.threads = threads or max(1, len(os.sched_getaffinity(0)))
         self.stats = np.zeros(7, dtype=np.uint64)
+        self.fast = fast
 
     def render(self, camera: Camera, spp: int, ignore_history: bool, chunks: int = 1, collect_stats: bool = False) -> None:
         """`chunks` successive reference render(camera, spp, ignore_history and c == 0) calls."""
         sc = self.scene
         tex = sc.texture_table()
         st = (C.c_uint64 * 7)() if collect_stats else None
-        rc = lib().or_render(sc.prims, sc.prim_count, sc.nodes, sc.node_count, C.byref(camera), sc.skybox, tex,
-                             len(sc.textures), self.width, self.height, self.row_offset, self.row_stride,
+        rc = lib(self.fast).or_render(sc.prims, sc.prim_count, sc.nodes, sc.node_count, C.byref(camera), sc.skybox, tex,
+                             len(sc.textures), self.width, self.height, self.band_rows, self.row_offset, self.row_stride,
                              fptr(self.accum), self.rng, spp, chunks, int(bool(ignore_history)), self.threads, st)
         if rc != 0:
             raise RuntimeError("oracle: BVH traversal stack overflow (reference UB)")
@@ -370,7 +386,7 @@ class OracleRenderer:
             self.frames += 1
 
     def rng_array(self) -> np.ndarray:
-        return np.frombuffer(bytes(self.rng), dtype=np.uint32).reshape(self.rows, self.width, 6)
+        return np.frombuffer(bytes(self.rng), dtype=np.uint32)[:self.rows * self.width * 6].reshape(self.rows, self.width, 6)
 
     def tonemap(self, frames: Optional[int] = None) -> np.ndarray:
         out = np.zeros((self.rows, self.width, 4), dtype=np.uint8)

@@ -138,17 +138,31 @@ class Scene:
 
 
 class Pathtracer:
-    """The reference's Pathtracer on one MI355X (or on the row tile y = row_offset + k * row_stride)."""
+    """The reference's Pathtracer on one MI355X, on a row-band tile of the image, or on several GPUs.
 
-    def __init__(self, width: int, height: int, device: int = 0, row_offset: int = 0, row_stride: int = 1) -> None:
+    Tiles: the image is cut into bands of `band_rows` rows and this object renders the bands
+    b = row_offset + k * row_stride (band_rows = 1: rows y = row_offset + k * row_stride).
+    `devices=[...]` spans several GPUs of this process (pt_group_*, RCCL gather): the image calls
+    (accum, get_hdr_image_data, get_image_data) then return the full image.
+    """
+
+    def __init__(self, width: int, height: int, device: int = 0, row_offset: int = 0, row_stride: int = 1,
+                 band_rows: int = 1, devices: Optional[Sequence[int]] = None) -> None:
         self._r = C.c_void_p()
-        N.check_host(N.host().pth_renderer_create(int(width), int(height), int(device), int(row_offset),
-                                                  int(row_stride), C.byref(self._r)))
+        if devices is not None:
+            devs = (C.c_int * len(devices))(*[int(d) for d in devices])
+            N.check_host(N.host().pth_renderer_create_group(int(width), int(height), len(devices), devs, int(band_rows),
+                                                            C.byref(self._r)))
+        else:
+            N.check_host(N.host().pth_renderer_create_banded(int(width), int(height), int(device), int(band_rows),
+                                                             int(row_offset), int(row_stride), C.byref(self._r)))
         self.width, self.height = int(width), int(height)
         self.device = int(device)
-        self.row_offset, self.row_stride = int(row_offset), int(row_stride)
+        self.row_offset, self.row_stride, self.band_rows = int(row_offset), int(row_stride), int(band_rows)
+        self.devices = list(devices) if devices is not None else None
         self.rows = int(N.host().pth_renderer_local_rows(self._r))
         self._ctx = N.host().pth_renderer_context(self._r)
+        self._group = N.host().pth_renderer_group(self._r)
 
     def close(self) -> None:
         if getattr(self, "_r", None):
@@ -195,10 +209,19 @@ class Pathtracer:
 
     # --- device-layer access (C ABI of pt_hip.h) ------------------------------------------------
     def accum(self) -> np.ndarray:
-        """Raw accumulation sums (rows x width x 4 float32)."""
+        """Raw accumulation sums (rows x width x 4 float32); the gathered full image for a group."""
         out = np.zeros((self.rows, self.width, 4), dtype=np.float32)
-        N.check_ctx(N.hip().pt_read_accum(self._ctx, out.ctypes.data_as(C.POINTER(C.c_float))), self._ctx)
+        if self._group:
+            N.check_group(N.hip().pt_group_read_accum(self._group, out.ctypes.data_as(C.POINTER(C.c_float))), self._group)
+        else:
+            N.check_ctx(N.hip().pt_read_accum(self._ctx, out.ctypes.data_as(C.POINTER(C.c_float))), self._ctx)
         return out
+
+    def gather(self) -> float:
+        """Group only: RCCL gather of every device's rows to devices[0]; returns its wall time in ms."""
+        ms = C.c_float(0.0)
+        N.check_group(N.hip().pt_group_gather(self._group, C.byref(ms)), self._group)
+        return float(ms.value)
 
     def rng_state(self) -> np.ndarray:
         out = np.zeros((self.rows, self.width, 6), dtype=np.uint32)

@@ -52,6 +52,8 @@ P = C.POINTER
 _HIP_SYMBOLS = {
     "pt_device_count": (C.c_int, [P(C.c_int)]),
     "pt_create": (C.c_int, [C.c_int, C.c_uint32, C.c_uint32, C.c_uint32, C.c_uint32, P(C.c_void_p)]),
+    "pt_create_banded": (C.c_int, [C.c_int, C.c_uint32, C.c_uint32, C.c_uint32, C.c_uint32, C.c_uint32, P(C.c_void_p)]),
+    "pt_band_rows": (C.c_uint32, [C.c_uint32, C.c_uint32, C.c_uint32, C.c_uint32]),
     "pt_destroy": (None, [C.c_void_p]),
     "pt_set_scene": (C.c_int, [C.c_void_p, P(PtBvhNode), C.c_uint32, P(PtHittable), C.c_uint32]),
     "pt_set_texture": (C.c_int, [C.c_void_p, C.c_uint32, P(C.c_float), C.c_uint32, C.c_uint32]),
@@ -69,6 +71,18 @@ _HIP_SYMBOLS = {
     "pt_set_kernel_variant": (C.c_int, [C.c_void_p, C.c_int]),
     "pt_set_schedule": (C.c_int, [C.c_void_p, C.c_int]),
     "pt_last_error": (C.c_char_p, [C.c_void_p]),
+    "pt_group_create": (C.c_int, [C.c_int, P(C.c_int), C.c_uint32, C.c_uint32, C.c_uint32, P(C.c_void_p)]),
+    "pt_group_destroy": (None, [C.c_void_p]),
+    "pt_group_size": (C.c_int, [C.c_void_p]),
+    "pt_group_context": (C.c_void_p, [C.c_void_p, C.c_int]),
+    "pt_group_set_scene": (C.c_int, [C.c_void_p, P(PtBvhNode), C.c_uint32, P(PtHittable), C.c_uint32]),
+    "pt_group_set_texture": (C.c_int, [C.c_void_p, C.c_uint32, P(C.c_float), C.c_uint32, C.c_uint32]),
+    "pt_group_set_skybox": (C.c_int, [C.c_void_p, C.c_uint32]),
+    "pt_group_render": (C.c_int, [C.c_void_p, P(PtCamera), C.c_uint32, C.c_uint32, C.c_int, P(C.c_float)]),
+    "pt_group_gather": (C.c_int, [C.c_void_p, P(C.c_float)]),
+    "pt_group_read_accum": (C.c_int, [C.c_void_p, P(C.c_float)]),
+    "pt_group_tonemap": (C.c_int, [C.c_void_p, C.c_uint32, P(C.c_uint8)]),
+    "pt_group_last_error": (C.c_char_p, [C.c_void_p]),
 }
 
 _HOST_SYMBOLS = {
@@ -91,6 +105,10 @@ _HOST_SYMBOLS = {
     "pth_camera_translate": (C.c_int, [P(PtCamera), C.c_float, C.c_float, C.c_float]),
     "pth_radians": (C.c_float, [C.c_float]),
     "pth_renderer_create": (C.c_int, [C.c_uint32, C.c_uint32, C.c_int, C.c_uint32, C.c_uint32, P(C.c_void_p)]),
+    "pth_renderer_create_banded": (C.c_int, [C.c_uint32, C.c_uint32, C.c_int, C.c_uint32, C.c_uint32, C.c_uint32,
+                                             P(C.c_void_p)]),
+    "pth_renderer_create_group": (C.c_int, [C.c_uint32, C.c_uint32, C.c_int, P(C.c_int), C.c_uint32, P(C.c_void_p)]),
+    "pth_renderer_gather_ms": (C.c_float, [C.c_void_p]),
     "pth_renderer_destroy": (None, [C.c_void_p]),
     "pth_renderer_load_scene": (C.c_int, [C.c_void_p, C.c_char_p, P(PtCamera)]),
     "pth_renderer_render": (C.c_int, [C.c_void_p, P(PtCamera), C.c_uint32, C.c_uint32, C.c_int]),
@@ -100,6 +118,7 @@ _HOST_SYMBOLS = {
     "pth_renderer_hdr": (P(C.c_float), [C.c_void_p]),
     "pth_renderer_image": (P(C.c_uint8), [C.c_void_p]),
     "pth_renderer_context": (C.c_void_p, [C.c_void_p]),
+    "pth_renderer_group": (C.c_void_p, [C.c_void_p]),
     "pth_write_png": (C.c_int, [C.c_char_p, C.c_uint32, C.c_uint32, P(C.c_uint8), C.c_int]),
     "pth_write_hdr": (C.c_int, [C.c_char_p, C.c_uint32, C.c_uint32, P(C.c_float), C.c_int]),
 }
@@ -149,6 +168,11 @@ def check_host(rc: int) -> None:
 def check_ctx(rc: int, ctx) -> None:
     if rc != PT_OK:
         raise PathtracerError(rc, (hip().pt_last_error(ctx) or b"").decode(errors="replace"))
+
+
+def check_group(rc: int, group) -> None:
+    if rc != PT_OK:
+        raise PathtracerError(rc, (hip().pt_group_last_error(group) or b"").decode(errors="replace"))
 
 
 def device_count() -> int:

@@ -1,6 +1,7 @@
 // `pathtracer` command line tool: the reference's headless renderer (src/main.cpp:22-295) on
 // MI355X.  Same options, defaults, messages and output semantics; additions:
-//   -gpus N        tile the image over N GPUs (rows interleaved; bit-identical to 1 GPU)
+//   -gpus N        render on N GPUs of this process (8-row bands interleaved over the devices,
+//                  RCCL gather to device 0; bit-identical to 1 GPU)
 //   -chunk N       samples per render() call of the headless loop (default 8, main.cpp:272)
 //   -single_launch run all render() calls of the loop in one kernel launch (bit-identical)
 // The windowed / interactive mode (-window, -enable_controls) is not supported.
@@ -9,7 +10,6 @@
 #include <cstdlib>
 #include <cstring>
 #include <memory>
-#include <thread>
 #include <vector>
 
 #include "pathtracer_amd.hpp"
@@ -80,7 +80,7 @@ static bool processArgs(int argc, char* argv[], Params& params, int& gpus)
         printf("%-30s Enables camera controls (not supported)\n", controlsOption);
         printf("%-30s Set filepath of output image\n", outputOption);
         printf("%-30s Save image as HDR instead of PNG\n", outputHdrOption);
-        printf("%-30s Render on N GPUs (image rows interleaved)\n", "-gpus");
+        printf("%-30s Render on N GPUs (row bands interleaved, RCCL gather)\n", "-gpus");
         printf("%-30s Samples per render() call (default 8)\n", "-chunk");
         printf("%-30s Run all render() calls in one kernel launch\n", "-single_launch");
         return false;
@@ -116,61 +116,43 @@ int main(int argc, char* argv[])
         return EXIT_FAILURE;
     }
     gpus = std::max(1, std::min(gpus, available));
-    std::vector<std::unique_ptr<Pathtracer>> tiles;
-    std::vector<Camera> cams;
-    for (int g = 0; g < gpus; ++g) {
-        tiles.emplace_back(new Pathtracer(params.m_width, params.m_height, g, (uint32_t)g, (uint32_t)gpus));
-        cams.push_back(loadScene(*tiles.back(), params));
+    // main.cpp:263 constructs one Pathtracer on device 0; -gpus N spans N devices with the same
+    // interface (row bands over the devices, RCCL gather to device 0 when the image is read)
+    std::unique_ptr<Pathtracer> pathtracer;
+    if (gpus == 1) {
+        pathtracer.reset(new Pathtracer(params.m_width, params.m_height));
+    } else {
+        std::vector<int> devices(gpus);
+        for (int g = 0; g < gpus; ++g) devices[g] = g;
+        pathtracer.reset(new Pathtracer(params.m_width, params.m_height, devices));
     }
+    Camera camera = loadScene(*pathtracer, params);
 
+    // headless loop (main.cpp:269-288)
     const uint32_t chunk = params.m_chunk;
-    std::vector<float> gpuTime(gpus, 0.0f);
-    auto renderTile = [&](int g) {
-        Pathtracer& pt = *tiles[g];
-        if (params.m_singleLaunch && params.m_spp > 0) {
-            const uint32_t full = params.m_spp / chunk, rest = params.m_spp % chunk;
-            if (full) { pt.renderChunks(cams[g], chunk, full, true); gpuTime[g] += pt.getTiming(); }
-            if (rest) { pt.renderChunks(cams[g], rest, 1, full == 0); gpuTime[g] += pt.getTiming(); }
-            return;
-        }
+    float totalGpuTime = 0.0f;
+    if (params.m_singleLaunch && params.m_spp > 0) {
+        const uint32_t full = params.m_spp / chunk, rest = params.m_spp % chunk;
+        if (full) { pathtracer->renderChunks(camera, chunk, full, true); totalGpuTime += pathtracer->getTiming(); }
+        if (rest) { pathtracer->renderChunks(camera, rest, 1, full == 0); totalGpuTime += pathtracer->getTiming(); }
+    } else {
         for (uint32_t i = 0; i < params.m_spp; i += chunk) {
             const uint32_t spp = std::min(i + chunk, params.m_spp) - i;
-            pt.render(cams[g], spp, i == 0);
-            gpuTime[g] += pt.getTiming();
-            if (g == 0 && i % (chunk * 4) == 0) printf("Accumulated %d samples\n", (int)i);
+            pathtracer->render(camera, spp, i == 0);
+            totalGpuTime += pathtracer->getTiming();
+            if (i % (chunk * 4) == 0) printf("Accumulated %d samples\n", (int)i);
         }
-    };
-    if (gpus == 1) renderTile(0);
-    else {
-        std::vector<std::thread> th;
-        for (int g = 0; g < gpus; ++g) th.emplace_back(renderTile, g);
-        for (auto& t : th) t.join();
     }
-    const float totalGpuTime = *std::max_element(gpuTime.begin(), gpuTime.end());
     printf("Finished accumulating %d samples in %f ms GPU time\n", (int)params.m_spp, totalGpuTime);
 
     if (params.m_outputFilepath) {
         printf("Writing result to %s\n", params.m_outputFilepath);
         const uint32_t W = params.m_width, H = params.m_height;
-        bool ok;
-        if (params.m_outputHdr) {
-            std::vector<float> img((size_t)W * H * 4);
-            for (int g = 0; g < gpus; ++g) {
-                const float* t = tiles[g]->getHDRImageData();
-                for (uint32_t k = 0; k < tiles[g]->localRows(); ++k)
-                    memcpy(&img[(size_t)(g + k * gpus) * W * 4], t + (size_t)k * W * 4, (size_t)W * 4 * sizeof(float));
-            }
-            ok = ptamd::writeHDR(params.m_outputFilepath, W, H, img.data(), true);
-        } else {
-            std::vector<uint8_t> img((size_t)W * H * 4);
-            for (int g = 0; g < gpus; ++g) {
-                const char* t = tiles[g]->getImageData();
-                for (uint32_t k = 0; k < tiles[g]->localRows(); ++k)
-                    memcpy(&img[(size_t)(g + k * gpus) * W * 4], t + (size_t)k * W * 4, (size_t)W * 4);
-            }
-            ok = ptamd::writePNG(params.m_outputFilepath, W, H, img.data(), true);
-        }
+        const bool ok = params.m_outputHdr
+                            ? ptamd::writeHDR(params.m_outputFilepath, W, H, pathtracer->getHDRImageData(), true)
+                            : ptamd::writePNG(params.m_outputFilepath, W, H, (const uint8_t*)pathtracer->getImageData(), true);
         if (!ok) printf("Failed to write file!\n");
+        if (gpus > 1) printf("Gathered %d GPU tiles over RCCL in %f ms\n", gpus, pathtracer->lastGatherMs());
     }
     return EXIT_SUCCESS;
 }

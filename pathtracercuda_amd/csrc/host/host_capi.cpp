@@ -228,6 +228,34 @@ PT_API int pth_renderer_create(uint32_t width, uint32_t height, int device, uint
     PTH_GUARD_END
 }
 
+PT_API int pth_renderer_create_banded(uint32_t width, uint32_t height, int device, uint32_t band_rows,
+                                      uint32_t band_offset, uint32_t band_stride, pth_renderer** out)
+{
+    if (!out) return setError(PT_ERR_ARG, "invalid argument");
+    *out = nullptr;
+    PTH_GUARD_BEGIN
+    auto r = std::make_unique<pth_renderer>();
+    r->pt = std::make_unique<Pathtracer>(width, height, Pathtracer::Tile{device, band_rows, band_offset, band_stride});
+    *out = r.release();
+    return PT_OK;
+    PTH_GUARD_END
+}
+
+PT_API int pth_renderer_create_group(uint32_t width, uint32_t height, int ndev, const int* devices, uint32_t band_rows,
+                                     pth_renderer** out)
+{
+    if (!out || ndev < 1 || !devices) return setError(PT_ERR_ARG, "invalid argument");
+    *out = nullptr;
+    PTH_GUARD_BEGIN
+    auto r = std::make_unique<pth_renderer>();
+    r->pt = std::make_unique<Pathtracer>(width, height, std::vector<int>(devices, devices + ndev), band_rows);
+    *out = r.release();
+    return PT_OK;
+    PTH_GUARD_END
+}
+
+PT_API float pth_renderer_gather_ms(const pth_renderer* r) { return r ? r->pt->lastGatherMs() : 0.0f; }
+
 PT_API void pth_renderer_destroy(pth_renderer* r) { delete r; }
 
 PT_API int pth_renderer_load_scene(pth_renderer* r, const char* path, pt_camera* camera)
@@ -290,6 +318,7 @@ PT_API const uint8_t* pth_renderer_image(pth_renderer* r)
 }
 
 PT_API pt_context* pth_renderer_context(pth_renderer* r) { return r ? r->pt->context() : nullptr; }
+PT_API pt_group* pth_renderer_group(pth_renderer* r) { return r ? r->pt->group() : nullptr; }
 
 PT_API int pth_write_png(const char* path, uint32_t w, uint32_t h, const uint8_t* rgba, int flip)
 {

@@ -21,6 +21,7 @@
 //     hit record is reconstructed once for the closest hit instead of for every candidate hit.
 #include <hip/hip_runtime.h>
 #include <rocprim/device/device_radix_sort.hpp>
+#include <rccl/rccl.h>
 #include <stdint.h>
 #include <string.h>
 #include <stdio.h>
@@ -28,6 +29,8 @@
 #include <vector>
 #include <algorithm>
 #include <atomic>
+#include <thread>
+#include <chrono>
 
 #include "pt_math.h"
 #include "../../include/pt_hip.h"
@@ -56,6 +59,7 @@ struct TraceParams {
     unsigned long long* stats;  // 6 counters (instrumented variant only)
     uint32_t skybox;
     uint32_t width, height, rowOffset, rowStride, rows;
+    uint32_t bandShift;         // rows are tiled in bands of 1 << bandShift rows (global_row)
     uint32_t spp, chunks, ignoreFirst;
     uint32_t tilesX, tilesY;
     uint32_t nodeCount, primCount, stackDepth, slabFast;
@@ -67,8 +71,19 @@ struct TraceParams {
     uint32_t* tileCursor;       // persistent variants: {next dispatch slot, waves finished}, rewound by the last wave
     uint32_t numSlots;          // dispatch slots = 8x8 tiles
     uint32_t* tileCost;         // per-tile shader-clock cycles of this launch (null: not recorded)
+    uint32_t discard;           // != 0: cost pre-pass -- pixel state (RNG, accum) is read, never written
     DevCamera cam;
 };
+
+// Row tiling of an image across contexts (multi-GPU): the image is cut into bands of
+// B = 1 << shift rows, and a context owns bands b = offset + k * stride.  Local row ly lies in the
+// context's band ly / B at row ly % B.  B = 1 is plain row interleaving (y = offset + ly * stride);
+// B = 8 keeps every 8x8 tile of a context a spatially coherent 8x8 tile of the image.  Seeds and
+// camera coordinates always use the global row, so every tiling reproduces the 1-GPU image.
+__host__ __device__ inline uint32_t global_row(uint32_t ly, uint32_t offset, uint32_t stride, uint32_t shift)
+{
+    return ((offset + (ly >> shift) * stride) << shift) + (ly & ((1u << shift) - 1u));
+}
 
 // ---------------------------------------------------------------------------------------------
 // texture sampling: CUDA 2-D linear fetch, normalised coordinates, wrap (u) / clamp (v),
@@ -216,87 +231,6 @@ PT_DEV bool prim_hit(const float4* __restrict__ prims, uint32_t p, f3 o, f3 d, f
     if (!v0 && !v1) return false;
     tOut = v0 ? t0 : t1;
     return true;
-}
-
-// prim_hit for mixed-type leaves, written for the scalar unit: each shape family present among the
-// wave's active lanes is evaluated for all of them behind a wave-uniform branch, and each lane
-// selects its own family's verdict.  A lane's arithmetic is prim_hit's, operation for operation;
-// the reject tests are the same comparisons, negated (so NaNs pass or fail exactly as there), and
-// lanes of other families only compute values that are discarded.  The wave issues the same VALU
-// for the families present, without a divergent if/else (exec save, flip, restore on the CU's one
-// scalar unit) per family, per guard and per test.
-PT_DEV bool prim_hit_u(const float4* __restrict__ prims, uint32_t p, f3 o, f3 d, float tMin, float tMax, float& tOut,
-                       bool act = true)     // act = false: the lane joins no family (its verdict is discarded)
-{
-    const float4 r0 = prims[4 * p + 0];
-    const float4 r1 = prims[4 * p + 1];
-    const float4 r2 = prims[4 * p + 2];
-    const uint32_t type = __float_as_uint(prims[4 * p + 3].x);
-    const LocalRay r = to_local(r0, r1, r2, o, d);
-    const bool planar = act & (type == DISK || type == QUAD);   // lanes with act = false join no family
-    const bool cube = act & (type == CUBE);
-    const bool quadric = act & (type != DISK) & (type != QUAD) & (type != CUBE);
-    bool hit = false;
-    float t = 0.0f;
-    if (__ballot(planar) != 0ull) {                         // Hittable.inl:205-235, 299-329
-        const float tp = -r.o.y / r.d.y;
-        const float hx = r.o.x + r.d.x * tp;
-        const float hz = r.o.z + r.d.z * tp;
-        const bool inQuad = !(fabsf(hx) > 1.0f || fabsf(hz) > 1.0f);
-        const bool inDisk = !((hx * hx + hz * hz) >= 1.0f);
-        const bool hp = planar & !(r.d.y == 0.0f) & !(tp <= tMin || tp > tMax) & (type == QUAD ? inQuad : inDisk);
-        t = hp ? tp : t;
-        hit = hp;
-    }
-    if (__ballot(cube) != 0ull) {                           // Hittable.inl:331-358, AABB.inl:46-69
-        float lo = tMin, hi = tMax;
-        const float ox[3] = {r.o.x, r.o.y, r.o.z};
-        const float dx[3] = {r.d.x, r.d.y, r.d.z};
-#pragma unroll
-        for (int a = 0; a < 3; ++a) {
-            const float invD = rcp_rn_u(dx[a]);
-            const float t0 = (-1.0f - ox[a]) * invD;
-            const float t1 = (1.0f - ox[a]) * invD;
-            const bool sw = invD < 0.0f;
-            const float n0 = sw ? t1 : t0, n1 = sw ? t0 : t1;
-            lo = n0 > lo ? n0 : lo;
-            hi = n1 < hi ? n1 : hi;
-        }
-        const bool hc = cube & !(hi <= lo);
-        t = hc ? lo : t;
-        hit = hit | hc;
-    }
-    if (__ballot(quadric) != 0ull) {                        // quadric_roots + Hittable.inl:147-297
-        const float B = (type == SPHERE) ? 1.0f : (type == CONE ? -1.0f : 0.0f);
-        const float Hc = (type == PARABOLOID) ? -1.0f : 0.0f;
-        const float J = (type == SPHERE || type == CYLINDER) ? -1.0f : 0.0f;
-        const f3 ro = r.o, rd = r.d;
-        const float a = (rd.x * rd.x + (B * rd.y) * rd.y) + rd.z * rd.z;
-        const float b = (((2.0f * ro.x) * rd.x + ((2.0f * B) * ro.y) * rd.y) + (2.0f * ro.z) * rd.z) + Hc * rd.y;
-        const float c = (((ro.x * ro.x + (B * ro.y) * ro.y) + ro.z * ro.z) + Hc * ro.y) + J;
-        const float disc = b * b - 4.0f * a * c;
-        const bool real = !(disc < 0.0f);
-        if (__ballot(quadric & real) != 0ull) {              // most tests end here: no real root
-        const float rt = sqrt_rn_u(real ? disc : 1.0f);     // discarded where !real
-        const float q = b < 0.0f ? -0.5f * (b - rt) : -0.5f * (b + rt);
-        const float x0 = q / a;
-        const float x1 = c / q;
-        const float t0 = x0 > x1 ? x1 : x0;
-        const float t1 = x0 > x1 ? x0 : x1;
-        const bool pass = quadric & real & !(t0 > tMax || t1 <= tMin);
-        const float h0 = rd.y * t0 + ro.y;
-        const float h1 = rd.y * t1 + ro.y;
-        const bool v0 = (t0 > tMin) & (t0 <= tMax) & (h0 >= -1.0f) & (h0 <= 1.0f);
-        const bool v1 = (t1 > tMin) & (t1 <= tMax) & (h1 >= -1.0f) & (h1 <= 1.0f);
-        const bool sph = type == SPHERE;
-        const bool hq = pass & (sph | v0 | v1);
-        const float tq = sph ? (t0 > tMin ? t0 : t1) : (v0 ? t0 : t1);
-        t = hq ? tq : t;
-        hit = hit | hq;
-        }
-    }
-    tOut = t;
-    return hit;
 }
 
 struct Counters {
@@ -685,9 +619,9 @@ struct TravState {
     float tMax;
 };
 
-// LEAN (WW = 100 * (LEAN + 1) + EXITQ): bit 0 -- walk_interior for the interior walk; bit 2 --
-// prim_hit_u (select form) for the primitive tests.  Results are identical for every LEAN.
-template <bool STATS, int EXITQ, int LEAN = 0>
+// The interior walk is walk_interior (the lean form: wave-uniform slab-form choice, unconditional
+// far-child write).  WW = 200 + EXITQ selects this traversal.
+template <bool STATS, int EXITQ>
 PT_DEV bool traverse_cb_phase(const float4* __restrict__ cnodes, const float4* __restrict__ prims, uint2* stack,
                               const TraceParams& P, f3 o, f3 d, bool fresh, TravState& ts, Counters& cnt)
 {
@@ -728,34 +662,17 @@ PT_DEV bool traverse_cb_phase(const float4* __restrict__ cnodes, const float4* _
         return false;
     };
     uint64_t tPhase = STATS ? __builtin_amdgcn_s_memtime() : 0;
-    const bool allFast = (LEAN & 1) && __ballot(!R.fast) == 0;          // wave-uniform
+    const bool allFast = __ballot(!R.fast) == 0;                         // wave-uniform
     while (!done) {
-        if (LEAN & 1) {
-            done = allFast ? walk_interior<STATS, true>(cnodes, stack, R, negMask, tMin, tMax, cur, sp, cnt)
-                           : walk_interior<STATS, false>(cnodes, stack, R, negMask, tMin, tMax, cur, sp, cnt);
-        } else {
-        while ((cur >> 24) == 0u) {                               // interior walk
-            if (STATS) { cnt.node_tests += 2; wave_tick(cnt.w_node); }
-            const ChildPair ch = cb_children(cnodes, cur, R, negMask, tMin, tMax);   // trace.cu:66-77
-            if (ch.both) {
-                stack[64u * sp] = make_uint2(ch.wF, __float_as_uint(ch.loF));
-                ++sp;
-            }
-            if (ch.any) {
-                cur = ch.wNext;
-            } else if (!pop()) {
-                done = true;
-                break;
-            }
-        }
-        }
+        done = allFast ? walk_interior<STATS, true>(cnodes, stack, R, negMask, tMin, tMax, cur, sp, cnt)
+                       : walk_interior<STATS, false>(cnodes, stack, R, negMask, tMin, tMax, cur, sp, cnt);
         if (STATS) wave_time(cnt.cyc_node, tPhase);
         if (done) break;
         uint32_t leafOff = cur & 0xffffffu, leafCnt = cur >> 24;
         while (leafCnt > 0) {
             if (STATS) { cnt.prim_tests++; wave_tick(cnt.w_prim); }
             float t;
-            if ((LEAN & 4) ? prim_hit_u(prims, leafOff, o, d, tMin, tMax, t) : prim_hit(prims, leafOff, o, d, tMin, tMax, t)) {
+            if (prim_hit(prims, leafOff, o, d, tMin, tMax, t)) {
                 tMax = t;
                 elem = leafOff;
             }
@@ -772,110 +689,6 @@ PT_DEV bool traverse_cb_phase(const float4* __restrict__ cnodes, const float4* _
     ts.elem = elem;
     ts.tMax = tMax;
     return done;
-}
-
-// ---------------------------------------------------------------------------------------------
-// Speculative child-box traversal (WW == 5).  While some lane of the wave still searches for its
-// next leaf, lanes that already hold one keep walking and queue a second leaf (Aila & Laine's
-// speculative traversal).  Exactness: child boxes are nested (a parent's bounds are the union of
-// its children's), so with the same ray the rounded slab values satisfy lo_child >= lo_parent;
-// walking with a stale (larger) t_max therefore visits a superset of the reference's nodes, in
-// the reference's order (near/far depend on the ray only), and finds a superset of its leaves in
-// order.  Leaves are tested strictly in that order and each is re-checked as t_max > lo with the
-// t_max of that moment -- exactly the reference's verdict for the leaf (an ancestor culled by the
-// reference has lo_anc <= lo_leaf, so the leaf fails the check too).  Per-lane node culling,
-// primitive tests and tie rules are the reference's; speculative node tests are extra work only.
-// ---------------------------------------------------------------------------------------------
-template <bool STATS>
-PT_DEV uint32_t traverse_spec(const float4* __restrict__ cnodes, const float4* __restrict__ prims, uint2* stack,
-                              const TraceParams& P, f3 o, f3 d, float& tHit, Counters& cnt)
-{
-    const float tMin = 0.001f;
-    float tMax = kFltMax;
-    SlabRay R;
-    R.o = o;
-    R.ix = rcp_rn(d.x);
-    R.iy = rcp_rn(d.y);
-    R.iz = rcp_rn(d.z);
-    R.fast = P.slabFast && __builtin_isfinite(R.ix) && __builtin_isfinite(R.iy) && __builtin_isfinite(R.iz);
-    R.ox2 = f2(o.x, o.x);
-    R.oy2 = f2(o.y, o.y);
-    R.oz2 = f2(o.z, o.z);
-    R.ix2 = f2(R.ix, R.ix);
-    R.iy2 = f2(R.iy, R.iy);
-    R.iz2 = f2(R.iz, R.iz);
-    const uint32_t negMask = (d.x < 0.0f ? 1u : 0u) | (d.y < 0.0f ? 2u : 0u) | (d.z < 0.0f ? 4u : 0u);
-    uint32_t sp = 0, elem = 0xffffffffu;
-    uint32_t cur = P.rootWord;
-    float curLo;
-    // leaf queue (FIFO, capacity 2): words and lo values
-    uint32_t qw0 = 0, qw1 = 0, qn = 0;
-    float ql0 = 0.0f, ql1 = 0.0f;
-    if (STATS) { cnt.node_tests++; wave_tick(cnt.w_node); }
-    float X;
-    curLo = slab_lo_x(R, f2(P.rootBox[0], P.rootBox[1]), f2(P.rootBox[2], P.rootBox[3]), f2(P.rootBox[4], P.rootBox[5]),
-                      tMin, X);
-    bool done = !(X > curLo && tMax > curLo);
-    uint64_t tPhase = STATS ? __builtin_amdgcn_s_memtime() : 0;
-    for (;;) {
-        // walk until every lane that can still walk holds a leaf; lanes holding one queue a second
-        for (;;) {
-            if (__ballot(!done && qn == 0) == 0ull) break;
-            if (!done && qn < 2u) {
-                if (cur >> 24) {                                   // leaf: queue it, pop the next
-                    if (qn == 0u) { qw0 = cur; ql0 = curLo; }
-                    else { qw1 = cur; ql1 = curLo; }
-                    ++qn;
-                    done = true;
-                    while (sp > 0) {
-                        const uint2 e = stack[64u * (--sp)];
-                        if (tMax > __uint_as_float(e.y)) { cur = e.x; curLo = __uint_as_float(e.y); done = false; break; }
-                    }
-                } else {
-                    if (STATS) { cnt.node_tests += 2; wave_tick(cnt.w_node); }
-                    const ChildPair ch = cb_children(cnodes, cur, R, negMask, tMin, tMax);
-                    if (ch.both) {
-                        stack[64u * sp] = make_uint2(ch.wF, __float_as_uint(ch.loF));
-                        ++sp;
-                    }
-                    if (ch.any) {
-                        cur = ch.wNext;
-                        curLo = ch.loNext;
-                    } else {
-                        done = true;
-                        while (sp > 0) {
-                            const uint2 e = stack[64u * (--sp)];
-                            if (tMax > __uint_as_float(e.y)) { cur = e.x; curLo = __uint_as_float(e.y); done = false; break; }
-                        }
-                    }
-                }
-            }
-        }
-        if (STATS) wave_time(cnt.cyc_node, tPhase);
-        if (qn == 0u) break;                                       // done and nothing queued
-        // oldest queued leaf, re-checked against the current t_max, primitives in order
-        const uint32_t w = qw0;
-        const float lo = ql0;
-        qw0 = qw1;
-        ql0 = ql1;
-        --qn;
-        if (tMax > lo) {
-            uint32_t leafOff = w & 0xffffffu, leafCnt = w >> 24;
-            while (leafCnt > 0) {
-                if (STATS) { cnt.prim_tests++; wave_tick(cnt.w_prim); }
-                float t;
-                if (prim_hit(prims, leafOff, o, d, tMin, tMax, t)) {
-                    tMax = t;
-                    elem = leafOff;
-                }
-                ++leafOff;
-                --leafCnt;
-            }
-        }
-        if (STATS) wave_time(cnt.cyc_leaf, tPhase);
-    }
-    tHit = tMax;
-    return elem;
 }
 
 // Surface data of the closest hit (Hittable.inl:126-144 + the shape's normal/uv), rebuilt once.
@@ -1005,7 +818,7 @@ struct PathState {
     f3 o, d;          // current ray
     f3 L, T;          // radiance and throughput of the current path (trace.cu:104-105)
     f3 color;         // sum of the finished paths of the current render() call (trace.cu:186)
-    uint32_t li;      // local pixel index: the accumulation value lives in P.accum[li]
+    float* acc;       // this lane's running accumulation value in LDS (x, y, z at acc[0], [64], [128])
     uint32_t s, c, bounce;
     bool alive;
 };
@@ -1133,22 +946,22 @@ PT_DEV bool shade(const TraceParams& P, const float4* __restrict__ prims, uint32
 }
 
 // End of a path: sum it into the render() call's color; at the end of a call fold the call into
-// the accumulation value (trace.cu:193-198); start the next sample while any remain.
+// the accumulation value (trace.cu:193-198); start the next sample while any remain.  The running
+// accumulation value lives in the wave's LDS slice for the whole launch (loaded by load_pixel,
+// stored once by store_pixel), so a launch of many render() calls writes each pixel once instead of
+// once per call -- the fold and its order (color + accum) are unchanged.
 template <bool STATS>
 PT_DEV void finish_path(const TraceParams& P, PathState& ps, Xorwow& rng, float fx, float fy, Counters& cnt)
 {
     ps.color = add(ps.color, ps.L);
     if (STATS) cnt.samples++;
     if (++ps.s == P.spp) {
-        // fold the call into the accumulation value (trace.cu:196-198); the value is read and
-        // written in global memory once per call rather than held in registers for the launch
         const bool ignore = (ps.c == 0) && P.ignoreFirst;
         f3 acc = ps.color;
-        if (!ignore) {
-            const float4 old = P.accum[ps.li];
-            acc = add(ps.color, mk(old.x, old.y, old.z));
-        }
-        P.accum[ps.li] = make_float4(acc.x, acc.y, acc.z, 1.0f);
+        if (!ignore) acc = add(ps.color, mk(ps.acc[0], ps.acc[64], ps.acc[128]));
+        ps.acc[0] = acc.x;
+        ps.acc[64] = acc.y;
+        ps.acc[128] = acc.z;
         ps.color = splat(0.0f);
         ps.s = 0;
         if (++ps.c == P.chunks) ps.alive = false;
@@ -1211,19 +1024,19 @@ PT_DEV PixelCtx pixel_of(const TraceParams& P, uint32_t tile, uint32_t lane)
         pc.li = pc.valid ? li : 0;
         const uint32_t ly = (uint32_t)(pc.li / P.width);
         pc.px = (uint32_t)(pc.li - (size_t)ly * P.width);
-        pc.py = P.rowOffset + ly * P.rowStride;
+        pc.py = global_row(ly, P.rowOffset, P.rowStride, P.bandShift);
         return pc;
     }
     const uint32_t tileX = tile % P.tilesX, tileY = tile / P.tilesX;
     pc.px = tileX * 8u + (lane & 7u);
     const uint32_t ly = tileY * 8u + (lane >> 3);
     pc.valid = tileY < P.tilesY && pc.px < P.width && ly < P.rows;
-    pc.py = P.rowOffset + ly * P.rowStride;
+    pc.py = global_row(ly, P.rowOffset, P.rowStride, P.bandShift);
     pc.li = (size_t)ly * P.width + pc.px;
     return pc;
 }
 
-PT_DEV void load_pixel(const TraceParams& P, const PixelCtx& pc, Xorwow& rng, PathState& ps)
+PT_DEV void load_pixel(const TraceParams& P, const PixelCtx& pc, Xorwow& rng, PathState& ps, float* accL)
 {
     rng.d = P.rng[pc.li];
     rng.v0 = P.rng[pc.npix + pc.li];
@@ -1231,7 +1044,13 @@ PT_DEV void load_pixel(const TraceParams& P, const PixelCtx& pc, Xorwow& rng, Pa
     rng.v2 = P.rng[3 * pc.npix + pc.li];
     rng.v3 = P.rng[4 * pc.npix + pc.li];
     rng.v4 = P.rng[5 * pc.npix + pc.li];
-    ps.li = (uint32_t)pc.li;
+    ps.acc = accL;
+    if (!P.ignoreFirst) {                        // the first call of an ignoreHistory launch overwrites it
+        const float4 a = P.accum[pc.li];
+        accL[0] = a.x;
+        accL[64] = a.y;
+        accL[128] = a.z;
+    }
     ps.color = splat(0.0f);
     ps.L = splat(0.0f);
     ps.T = splat(1.0f);
@@ -1247,6 +1066,7 @@ PT_DEV void store_pixel(const TraceParams& P, const PixelCtx& pc, const Xorwow& 
     P.rng[3 * pc.npix + pc.li] = rng.v2;
     P.rng[4 * pc.npix + pc.li] = rng.v3;
     P.rng[5 * pc.npix + pc.li] = rng.v4;
+    P.accum[pc.li] = make_float4(ps.acc[0], ps.acc[64], ps.acc[128], 1.0f);   // trace.cu:198, once per launch
 }
 
 // ---------------------------------------------------------------------------------------------
@@ -1275,9 +1095,12 @@ __global__ void __launch_bounds__(WPB * 64, MINW) trace_kernel(TraceParams P)
     }
     const float4* __restrict__ nodes = SL >= 1 ? lds4 : gnodes;
     const float4* __restrict__ prims = SL >= 2 ? lds4 + nodeF4 : P.prims;
-    // wave stacks: stackDepth x 64 entries of u32 (node index), or of uint2 (word, lo) for WW == 3
-    uint32_t* stack = reinterpret_cast<uint32_t*>(lds4 + sceneF4) + (WW >= 3 ? 2u : 1u) * wave * P.stackDepth * 64u +
-                      (WW >= 3 ? 2u : 1u) * lane;
+    // wave stacks: stackDepth x 64 entries of u32 (node index), or of uint2 (word, lo) for WW >= 3;
+    // then one accumulation slice per wave (3 planes of 64 floats)
+    uint32_t* ldsStacks = reinterpret_cast<uint32_t*>(lds4 + sceneF4);
+    const uint32_t stackWords = (WW >= 3 ? 2u : 1u) * P.stackDepth * 64u;
+    uint32_t* stack = ldsStacks + wave * stackWords + (WW >= 3 ? 2u : 1u) * lane;
+    float* accL = reinterpret_cast<float*>(ldsStacks + WPB * stackWords) + wave * 192u + lane;
     Counters cnt = {};
     uint32_t slot = PERSIST ? wave_fetch(P.tileCursor, 1u) : blockIdx.x * (uint32_t)WPB + wave;
     for (;;) {
@@ -1288,7 +1111,7 @@ __global__ void __launch_bounds__(WPB * 64, MINW) trace_kernel(TraceParams P)
     if (pc.valid) {
         Xorwow rng;
         PathState ps;
-        load_pixel(P, pc, rng, ps);
+        load_pixel(P, pc, rng, ps, accL);
         const float fx = (float)(int32_t)pc.px, fy = (float)(int32_t)pc.py;
         camera_ray(P, fx, fy, rng, ps.o, ps.d);
         uint64_t tAll = STATS ? __builtin_amdgcn_s_memtime() : 0;
@@ -1298,7 +1121,7 @@ __global__ void __launch_bounds__(WPB * 64, MINW) trace_kernel(TraceParams P)
             TravState ts = {0u, 0u, 0xffffffffu, kFltMax};
             while (ps.alive) {
                 if (STATS && fresh) { cnt.segments++; wave_tick(cnt.w_segments); }
-                const bool tdone = traverse_cb_phase<STATS, WW % 100, WW / 100 - 1>(nodes, prims, reinterpret_cast<uint2*>(stack), P,
+                const bool tdone = traverse_cb_phase<STATS, WW % 100>(nodes, prims, reinterpret_cast<uint2*>(stack), P,
                                                                         ps.o, ps.d, fresh, ts, cnt);
                 fresh = tdone;
                 if (!tdone) continue;                              // suspended: resumes next round
@@ -1311,8 +1134,7 @@ __global__ void __launch_bounds__(WPB * 64, MINW) trace_kernel(TraceParams P)
         while (WW < 100 && ps.alive) {
             if (STATS) { cnt.segments++; wave_tick(cnt.w_segments); }
             float t;
-            const uint32_t e = WW == 5 ? traverse_spec<STATS>(nodes, prims, reinterpret_cast<uint2*>(stack), P, ps.o, ps.d, t, cnt)
-                             : WW >= 3 ? traverse_cb<STATS>(nodes, prims, reinterpret_cast<uint2*>(stack), P, ps.o, ps.d, t, cnt)
+            const uint32_t e = WW >= 3 ? traverse_cb<STATS>(nodes, prims, reinterpret_cast<uint2*>(stack), P, ps.o, ps.d, t, cnt)
                                        : traverse<STATS, WW>(nodes, prims, stack, ps.o, ps.d, P.slabFast != 0, t, cnt);
             uint64_t tS = STATS ? __builtin_amdgcn_s_memtime() : 0;
             if (shade<STATS>(P, prims, e, t, ps, rng, cnt)) finish_path<STATS>(P, ps, rng, fx, fy, cnt);
@@ -1320,7 +1142,7 @@ __global__ void __launch_bounds__(WPB * 64, MINW) trace_kernel(TraceParams P)
         }
         if (STATS && WW >= 100 && tDone) cnt.cyc_lane_idle += __builtin_amdgcn_s_memtime() - tDone;
         if (STATS) wave_time(cnt.cyc_total, tAll);
-        store_pixel(P, pc, rng, ps);
+        if (!P.discard) store_pixel(P, pc, rng, ps);
     }
     if (P.tileCost && lane == 0 && tile < P.tilesX * P.tilesY)
         P.tileCost[tile] = (uint32_t)min(__builtin_amdgcn_s_memtime() - tWave, (uint64_t)0xffffffffu);
@@ -1338,119 +1160,16 @@ __global__ void __launch_bounds__(WPB * 64, MINW) trace_kernel(TraceParams P)
     flush_counters<STATS>(P, cnt);
 }
 
-// ---------------------------------------------------------------------------------------------
-// Kernel B: wave-scheduled state machine.  Every lane is in one of NODE (walking interior
-// nodes), LEAF (testing the primitives of a leaf, one per step), SHADE (traversal finished) or
-// DONE.  Each iteration the wave counts its lanes per state with __ballot and runs exactly one
-// phase for the lanes in that state: shading once SHADE_T lanes wait for it (or nothing else is
-// left), leaf tests once LEAF_T lanes wait (or no lane is walking nodes), node steps otherwise.
-// Every lane still performs the reference's sequence of node tests, primitive tests and shading
-// steps in order -- only the interleaving across lanes changes -- so results are bit-identical.
-// ---------------------------------------------------------------------------------------------
-enum : uint32_t { ST_NODE = 0, ST_LEAF = 1, ST_SHADE = 2, ST_DONE = 3 };
-
-template <bool STATS, int MINW, int SHADE_T, int LEAF_T>
-__global__ void __launch_bounds__(256, MINW) trace_sched_kernel(TraceParams P)
-{
-    extern __shared__ float4 lds4[];
-    const uint32_t lane = threadIdx.x & 63u;
-    const uint32_t wave = threadIdx.x >> 6;
-    const float4* __restrict__ nodes = P.nodes;
-    const float4* __restrict__ prims = P.prims;
-    uint32_t* stack = reinterpret_cast<uint32_t*>(lds4) + wave * P.stackDepth * 64u + lane;
-    const PixelCtx pc = pixel_of(P, blockIdx.x * 4u + wave, lane);
-    Counters cnt = {};
-    Xorwow rng = {};
-    PathState ps = {};
-    const float fx = (float)(int32_t)pc.px, fy = (float)(int32_t)pc.py;
-    const float tMin = 0.001f;
-    // traversal state (hitBVH, trace.cu:28-98)
-    float tMax = kFltMax, ix = 0.0f, iy = 0.0f, iz = 0.0f;
-    uint32_t cur = 0, sp = 0, elem = 0xffffffffu, leafOff = 0, leafCnt = 0, negMask = 0;
-    uint32_t state = ST_DONE;
-    if (pc.valid) {
-        load_pixel(P, pc, rng, ps);
-        if (ps.alive) {
-            camera_ray(P, fx, fy, rng, ps.o, ps.d);
-            state = ST_NODE;
-        }
-    }
-    bool fresh = true;   // a new ray needs its traversal set up
-    while (true) {
-        if (state == ST_NODE && fresh) {
-            ix = rcp_rn(ps.d.x);
-            iy = rcp_rn(ps.d.y);
-            iz = rcp_rn(ps.d.z);
-            negMask = (ps.d.x < 0.0f ? 1u : 0u) | (ps.d.y < 0.0f ? 2u : 0u) | (ps.d.z < 0.0f ? 4u : 0u);
-            tMax = kFltMax;
-            cur = 0;
-            sp = 0;
-            elem = 0xffffffffu;
-            fresh = false;
-            if (STATS) { cnt.segments++; wave_tick(cnt.w_segments); }
-        }
-        const unsigned long long mN = __ballot(state == ST_NODE);
-        const unsigned long long mL = __ballot(state == ST_LEAF);
-        const unsigned long long mS = __ballot(state == ST_SHADE);
-        if ((mN | mL | mS) == 0ull) break;
-        const int nN = __popcll(mN), nL = __popcll(mL), nS = __popcll(mS);
-        if (nS >= SHADE_T || (nN + nL) == 0) {
-            if (state == ST_SHADE) {
-                if (shade<STATS>(P, prims, elem, tMax, ps, rng, cnt)) finish_path<STATS>(P, ps, rng, fx, fy, cnt);
-                state = ps.alive ? ST_NODE : ST_DONE;
-                fresh = true;
-            }
-        } else if (nL >= LEAF_T || nN == 0) {
-            if (state == ST_LEAF) {
-                if (STATS) { cnt.prim_tests++; wave_tick(cnt.w_prim); }
-                float t;
-                if (prim_hit(prims, leafOff, ps.o, ps.d, tMin, tMax, t)) {
-                    tMax = t;
-                    elem = leafOff;
-                }
-                ++leafOff;
-                if (--leafCnt == 0) {
-                    if (sp == 0) state = ST_SHADE;
-                    else { cur = stack[64u * (--sp)]; state = ST_NODE; }
-                }
-            }
-        } else {
-            if (state == ST_NODE) {
-                if (STATS) { cnt.node_tests++; wave_tick(cnt.w_node); }
-                const NodeHit nh = node_test(nodes, cur, ps.o, ix, iy, iz, tMin, tMax);
-                if (nh.hit) {
-                    const uint32_t count = nh.pca >> 16;
-                    if (count > 0) {
-                        leafOff = nh.offset;
-                        leafCnt = count;
-                        state = ST_LEAF;
-                    } else {
-                        const uint32_t axis = (nh.pca >> 8) & 0xffu;
-                        const bool isNeg = (negMask >> axis) & 1u;
-                        stack[64u * (sp++)] = isNeg ? (cur + 1) : nh.offset;
-                        cur = isNeg ? nh.offset : (cur + 1);
-                    }
-                } else {
-                    if (sp == 0) state = ST_SHADE;
-                    else cur = stack[64u * (--sp)];
-                }
-            }
-        }
-    }
-    if (pc.valid) store_pixel(P, pc, rng, ps);
-    flush_counters<STATS>(P, cnt);
-}
-
 // initRandState (initRandState.cu:4-17): curand_init(1984 + x + y * width, 0, 0)
 __global__ void __launch_bounds__(256) init_rng_kernel(uint32_t* rng, uint32_t width, uint32_t rows, uint32_t rowOffset,
-                                                       uint32_t rowStride)
+                                                       uint32_t rowStride, uint32_t bandShift)
 {
     const size_t npix = (size_t)rows * width;
     const size_t li = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (li >= npix) return;
     const uint32_t x = (uint32_t)(li % width);
     const uint32_t ly = (uint32_t)(li / width);
-    const uint32_t y = rowOffset + ly * rowStride;
+    const uint32_t y = global_row(ly, rowOffset, rowStride, bandShift);
     const uint32_t idx = x + y * width;
     const Xorwow s = xorwow_init((uint64_t)(uint32_t)(1984u + idx));
     rng[li] = s.d;
@@ -1481,6 +1200,20 @@ __global__ void __launch_bounds__(256) tonemap_kernel(uchar4* out, const float4*
     out[i] = make_uchar4(q[0], q[1], q[2], 255);
 }
 
+// Multi-device gather, second half: scatter one device's received rows (its bands, in local row
+// order) into the full image.  A band is band-rows consecutive image rows in both buffers, so every
+// lane copies one float4 of a coalesced row.
+__global__ void __launch_bounds__(256) unpermute_rows_kernel(float4* __restrict__ full, const float4* __restrict__ part,
+                                                             uint32_t width, uint32_t rows, uint32_t offset,
+                                                             uint32_t stride, uint32_t shift)
+{
+    const size_t li = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (li >= (size_t)rows * width) return;
+    const uint32_t ly = (uint32_t)(li / width);
+    const uint32_t x = (uint32_t)(li - (size_t)ly * width);
+    full[(size_t)global_row(ly, offset, stride, shift) * width + x] = part[li];
+}
+
 } // namespace
 
 // =============================================================================================
@@ -1490,7 +1223,7 @@ struct pt_context {
     int device = 0;
     hipStream_t stream = nullptr;
     hipEvent_t ev0 = nullptr, ev1 = nullptr;
-    uint32_t width = 0, height = 0, rowOffset = 0, rowStride = 1, rows = 0;
+    uint32_t width = 0, height = 0, rowOffset = 0, rowStride = 1, rows = 0, bandShift = 0;
     float4* accum = nullptr;
     uint32_t* rng = nullptr;
     float4* nodes = nullptr;
@@ -1558,7 +1291,7 @@ static hipError_t launch_one(const TraceParams& P, hipStream_t stream)
 {
     const size_t nodeF4 = WW >= 3 ? 4 * (size_t)P.cnodeCount : 2 * (size_t)P.nodeCount;
     const size_t sceneBytes = ((SL >= 1 ? nodeF4 : 0) + (SL >= 2 ? 4 * (size_t)P.primCount : 0)) * sizeof(float4);
-    const size_t lds = sceneBytes + (size_t)WPB * P.stackDepth * 64 * (WW >= 3 ? 8 : 4);
+    const size_t lds = sceneBytes + (size_t)WPB * P.stackDepth * 64 * (WW >= 3 ? 8 : 4) + (size_t)WPB * 64 * 12;
     if (WW >= 3 && P.cnodes == nullptr) return launch_one<STATS, SL, WPB, 1, MINW, PERSIST>(P, stream);  // no child-box layout
     if (lds > 160 * 1024) {
         // scene too large to stage in LDS: the same variant reading the scene through the caches
@@ -1601,69 +1334,41 @@ static hipError_t launch_one(const TraceParams& P, hipStream_t stream)
     return hipGetLastError();
 }
 
-template <bool STATS, int MINW, int SHADE_T, int LEAF_T>
-static hipError_t launch_sched(const TraceParams& P, hipStream_t stream)
-{
-    const size_t lds = (size_t)4 * P.stackDepth * 64 * sizeof(uint32_t);
-    const uint32_t tiles = P.tilesX * P.tilesY;
-    const unsigned blocks = (tiles + 3) / 4;
-    trace_sched_kernel<STATS, MINW, SHADE_T, LEAF_T><<<blocks, 256, lds, stream>>>(P);
-    return hipGetLastError();
-}
-
+// Shipped variants (all bit-identical).  Measured-and-rejected variants of earlier rounds (single
+// loop with LDS nodes, other exit thresholds, 2/8/16-wave groups, 6-8 waves/SIMD, speculative
+// traversal, select-form primitive tests, a ballot-driven phase scheduler) are recorded in DESIGN.md
+// and git history, not shipped.
+//   1   reference control flow (one loop, node at a time), scene read through the caches
+//   4   node-at-a-time while-while, caches, 5 waves/SIMD   (scenes outside the child-box encoding)
+//   6   node-at-a-time while-while, nodes in LDS           (idem, small BVH)
+//   20  child-box traversal, one tile per wave             (counts the reference's node/prim tests)
+//   40  default: resumable lean child-box walk, records in LDS, persistent waves, exit <= 24/64
+//   41  default for cache-read scenes: same, records through the caches, exit <= 12/64
+//   46  default for deep cache-read BVHs: variant 41 compiled for 4 waves/SIMD (128 VGPRs)
 template <bool STATS>
 static hipError_t launch_variant(int v, const TraceParams& P, hipStream_t stream)
 {
     switch (v) {
     case 1: return launch_one<STATS, 0, 4, 0, 1>(P, stream);
-    case 2: return launch_one<STATS, 1, 4, 0, 1>(P, stream);
-    case 3: return launch_one<STATS, 0, 4, 1, 1>(P, stream);
     case 4: return launch_one<STATS, 0, 4, 1, 5>(P, stream);
-    case 5: return launch_one<STATS, 1, 4, 1, 1>(P, stream);
     case 6: return launch_one<STATS, 1, 4, 1, 5>(P, stream);
-    case 7: return launch_one<STATS, 1, 4, 0, 5>(P, stream);
-    case 8: return launch_one<STATS, 2, 8, 1, 5>(P, stream);
-    case 9: return launch_sched<STATS, 1, 32, 16>(P, stream);
-    case 10: return launch_one<STATS, 2, 16, 1, 5>(P, stream);
-    case 11: return launch_one<STATS, 1, 8, 1, 5>(P, stream);
-    case 12: return launch_one<STATS, 1, 4, 1, 6>(P, stream);
-    case 13: return launch_one<STATS, 1, 4, 1, 7>(P, stream);
-    case 14: return launch_one<STATS, 1, 4, 1, 8>(P, stream);
-    case 15: return launch_one<STATS, 0, 4, 1, 6>(P, stream);
-    case 16: return launch_one<STATS, 1, 4, 3, 6>(P, stream);
-    case 17: return launch_one<STATS, 0, 4, 3, 6>(P, stream);
-    case 18: return launch_one<STATS, 1, 8, 3, 6>(P, stream);
-    case 19: return launch_one<STATS, 1, 4, 3, 5>(P, stream);
     case 20: return launch_one<STATS, 0, 4, 3, 5>(P, stream);
-    case 21: return launch_one<STATS, 1, 4, 5, 5>(P, stream);
-    case 22: return launch_one<STATS, 0, 4, 5, 5>(P, stream);
-    case 23: return launch_one<STATS, 1, 4, 116, 5>(P, stream);  // resumable: exit at <= 16/64 walking
-    case 24: return launch_one<STATS, 1, 4, 104, 5>(P, stream);  // <= 4/64
-    case 25: return launch_one<STATS, 1, 4, 108, 5>(P, stream);  // <= 8/64
-    case 26: return launch_one<STATS, 0, 4, 108, 5>(P, stream);
-    case 27: return launch_one<STATS, 1, 4, 102, 5>(P, stream);  // <= 2/64
-    case 28: return launch_one<STATS, 1, 4, 112, 5>(P, stream);  // <= 12/64
-    case 29: return launch_one<STATS, 1, 4, 108, 6>(P, stream);
-    case 30: return launch_one<STATS, 1, 4, 112, 5, true>(P, stream);     // persistent waves
-    case 31: return launch_one<STATS, 0, 4, 108, 5, true>(P, stream);
-    case 32: return launch_one<STATS, 1, 8, 112, 5, true>(P, stream);
-    case 33: return launch_one<STATS, 1, 2, 112, 5, true>(P, stream);
-    case 34: return launch_one<STATS, 0, 4, 112, 5, true>(P, stream);
-    case 35: return launch_one<STATS, 1, 4, 104, 5, true>(P, stream);
-    case 36: return launch_one<STATS, 1, 4, 112, 6, true>(P, stream);
-    case 37: return launch_one<STATS, 1, 4, 120, 5, true>(P, stream);
-    case 38: return launch_one<STATS, 1, 4, 116, 5, true>(P, stream);
-    case 39: return launch_one<STATS, 0, 4, 116, 5, true>(P, stream);
-    case 40: return launch_one<STATS, 1, 4, 224, 5, true>(P, stream);     // lean interior walk, exit at <= 24/64
-    case 41: return launch_one<STATS, 0, 4, 212, 5, true>(P, stream);     // cache-read scene: exit at <= 12/64
-    case 42: return launch_one<STATS, 1, 4, 612, 5, true>(P, stream);     // + select-form primitive test
-    case 43: return launch_one<STATS, 0, 4, 612, 5, true>(P, stream);
-    case 44: return launch_one<STATS, 1, 4, 212, 5, true>(P, stream);     // lean walk, exit at <= 12/64
-    case 45: return launch_one<STATS, 0, 4, 224, 5, true>(P, stream);
-    case 46: return launch_one<STATS, 0, 4, 212, 4, true>(P, stream);     // deep cache-read BVH: LDS stacks allow 4 waves/SIMD, 128 VGPRs
-    default: return launch_one<STATS, 0, 4, 1, 1>(P, stream);
+    case 40: return launch_one<STATS, 1, 4, 224, 5, true>(P, stream);
+    case 41: return launch_one<STATS, 0, 4, 212, 5, true>(P, stream);
+    case 46: return launch_one<STATS, 0, 4, 212, 4, true>(P, stream);
+    default: return hipErrorInvalidValue;
     }
 }
+
+static bool variant_shipped(int v)
+{
+    return v == 0 || v == 1 || v == 4 || v == 6 || v == 20 || v == 40 || v == 41 || v == 46;
+}
+
+// Cost pre-pass of a cold-start launch (render_impl): samples per pixel, and the smallest launch
+// (spp x chunks) that gets one.
+constexpr uint32_t kPrepassSpp = 2;
+constexpr uint64_t kPrepassMinSpp = 16;
 
 static int pick_variant(const pt_context* ctx)
 {
@@ -1680,8 +1385,8 @@ static int pick_variant(const pt_context* ctx)
     // workgroups per CU (BVH depth > 16) runs at 4 waves/SIMD anyway: variant 46 is variant 41
     // compiled for that occupancy (128 VGPRs, no spill), +1% on the 100k-object scene (depth 19).
     const size_t cbBytes = 4 * (size_t)ctx->cnodeCount * sizeof(float4);
-    const size_t stackBytes = 4 * (size_t)ctx->stackDepth * 64 * 8;
-    if (ctx->cnodes) return cbBytes <= 48 * 1024 ? 40 : (5 * stackBytes > 160 * 1024 ? 46 : 41);
+    const size_t groupBytes = 4 * (size_t)ctx->stackDepth * 64 * 8 + 4 * 64 * 12;   // stacks + accumulation slices
+    if (ctx->cnodes) return cbBytes <= 48 * 1024 ? 40 : (5 * groupBytes > 160 * 1024 ? 46 : 41);
     const size_t nodeBytes = 2 * (size_t)ctx->nodeCount * sizeof(float4);
     return nodeBytes <= 48 * 1024 ? 6 : 4;
 }
@@ -1697,11 +1402,29 @@ PT_API int pt_device_count(int* count)
     return PT_OK;
 }
 
+PT_API uint32_t pt_band_rows(uint32_t height, uint32_t band_rows, uint32_t band_offset, uint32_t band_stride)
+{
+    if (band_rows == 0 || band_stride == 0 || (band_rows & (band_rows - 1)) != 0) return 0;
+    const uint32_t nb = (height + band_rows - 1) / band_rows;
+    if (band_offset >= nb) return 0;
+    const uint32_t own = (nb - band_offset + band_stride - 1) / band_stride;
+    const uint32_t last = band_offset + (own - 1) * band_stride;
+    return (own - 1) * band_rows + std::min(band_rows, height - last * band_rows);
+}
+
 PT_API int pt_create(int device, uint32_t width, uint32_t height, uint32_t row_offset, uint32_t row_stride,
                      pt_context** out)
 {
-    if (!out || width == 0 || height == 0 || row_stride == 0) return PT_ERR_ARG;
+    return pt_create_banded(device, width, height, 1, row_offset, row_stride, out);
+}
+
+PT_API int pt_create_banded(int device, uint32_t width, uint32_t height, uint32_t band_rows, uint32_t band_offset,
+                            uint32_t band_stride, pt_context** out)
+{
+    if (!out || width == 0 || height == 0 || band_stride == 0) return PT_ERR_ARG;
     *out = nullptr;
+    if (band_rows == 0 || band_rows > 256 || (band_rows & (band_rows - 1)) != 0) return PT_ERR_ARG;
+    const uint32_t row_offset = band_offset, row_stride = band_stride;
     int n = 0;
     if (hipGetDeviceCount(&n) != hipSuccess || n == 0) return PT_ERR_NO_DEVICE;
     if (device < 0 || device >= n) return PT_ERR_ARG;
@@ -1711,7 +1434,8 @@ PT_API int pt_create(int device, uint32_t width, uint32_t height, uint32_t row_o
     ctx->height = height;
     ctx->rowOffset = row_offset;
     ctx->rowStride = row_stride;
-    ctx->rows = row_offset < height ? (height - row_offset + row_stride - 1) / row_stride : 0;
+    ctx->bandShift = (uint32_t)__builtin_ctz(band_rows);
+    ctx->rows = pt_band_rows(height, band_rows, band_offset, band_stride);
     auto bail = [&](int code) { pt_destroy(ctx); return code; };
     if (hipSetDevice(device) != hipSuccess) return bail(PT_ERR_HIP);
     if (hipStreamCreateWithFlags(&ctx->stream, hipStreamNonBlocking) != hipSuccess) return bail(PT_ERR_HIP);
@@ -1727,7 +1451,8 @@ PT_API int pt_create(int device, uint32_t width, uint32_t height, uint32_t row_o
         return bail(PT_ERR_HIP);
     if (npix) {
         const unsigned blocks = (unsigned)((npix + 255) / 256);
-        init_rng_kernel<<<blocks, 256, 0, ctx->stream>>>(ctx->rng, width, ctx->rows, row_offset, row_stride);
+        init_rng_kernel<<<blocks, 256, 0, ctx->stream>>>(ctx->rng, width, ctx->rows, row_offset, row_stride,
+                                                                ctx->bandShift);
         if (hipGetLastError() != hipSuccess) return bail(PT_ERR_HIP);
     }
     if (hipStreamSynchronize(ctx->stream) != hipSuccess) return bail(PT_ERR_HIP);
@@ -1940,6 +1665,7 @@ static int render_impl(pt_context* ctx, const pt_camera* cam, uint32_t spp, uint
     P.rowOffset = ctx->rowOffset;
     P.rowStride = ctx->rowStride;
     P.rows = ctx->rows;
+    P.bandShift = ctx->bandShift;
     P.spp = spp;
     P.chunks = chunks;
     P.ignoreFirst = ignore ? 1u : 0u;
@@ -2012,6 +1738,25 @@ static int render_impl(pt_context* ctx, const pt_camera* cam, uint32_t spp, uint
     if (stats) PT_HIP_CHECK(ctx, hipMemsetAsync(ctx->stats, 0, 16 * sizeof(unsigned long long), ctx->stream));
     PT_HIP_CHECK(ctx, hipEventRecord(ctx->ev0, ctx->stream));
     const int variant = pick_variant(ctx);
+    if (sorted && (ctx->orderStale || !ctx->orderValid) && (uint64_t)spp * chunks >= kPrepassMinSpp && !stats) {
+        // Cold start (first launch, or the scene, a texture or the camera changed): a short cost
+        // pre-pass measures every tile -- kPrepassSpp samples per pixel from the pixels' current RNG
+        // state, nothing written back (discard) -- and the launch below already runs in cost order.
+        // Progressive 1-spp frames skip it and reuse the previous order for one launch instead.
+        TraceParams Q = P;
+        Q.spp = kPrepassSpp;
+        Q.chunks = 1;
+        Q.ignoreFirst = 1;
+        Q.discard = 1;
+        Q.order = nullptr;
+        PT_HIP_CHECK(ctx, launch_variant<false>(variant, Q, ctx->stream));
+        size_t bytes = ctx->sortTempBytes;
+        PT_HIP_CHECK(ctx, rocprim::radix_sort_pairs_desc(ctx->sortTemp, bytes, ctx->tileCost, ctx->sortKeys, ctx->tileIds,
+                                                         ctx->order, tiles, 0, 32, ctx->stream));
+        ctx->orderValid = true;
+        ctx->orderStale = false;
+        P.order = ctx->order;
+    }
     PT_HIP_CHECK(ctx, stats ? launch_variant<true>(variant, P, ctx->stream) : launch_variant<false>(variant, P, ctx->stream));
     PT_HIP_CHECK(ctx, hipGetLastError());
     PT_HIP_CHECK(ctx, hipEventRecord(ctx->ev1, ctx->stream));
@@ -2150,11 +1895,231 @@ PT_API uint32_t pt_local_rows(const pt_context* ctx) { return ctx ? ctx->rows : 
 
 PT_API int pt_set_kernel_variant(pt_context* ctx, int variant)
 {
-    if (!ctx || variant < 0 || variant > 46) return PT_ERR_ARG;
+    if (!ctx) return PT_ERR_ARG;
+    if (!variant_shipped(variant)) return fail(ctx, PT_ERR_ARG, "pt_set_kernel_variant: not a shipped variant");
     ctx->variant = variant;
     return PT_OK;
 }
 
 PT_API const char* pt_last_error(const pt_context* ctx) { return ctx ? ctx->err.c_str() : "null context"; }
+
+} // extern "C"
+
+// =============================================================================================
+// Multi-device group: one context per device over interleaved row bands, one RCCL communicator
+// per device (ncclCommInitAll, single process), and the framebuffer gather -- each device sends
+// its rows to device 0 with grouped ncclSend/ncclRecv over xGMI, device 0 scatters them into the
+// full image (unpermute_rows_kernel).  Replaces the reference's single hard-coded device
+// (Pathtracer.cpp:40) behind the same Pathtracer interface (include/pathtracer_amd.hpp).
+// =============================================================================================
+struct pt_group {
+    std::vector<int> devices;
+    std::vector<pt_context*> ctx;
+    std::vector<ncclComm_t> comms;
+    std::vector<size_t> stageOff;     // float4 offset of each device's rows in `stage`
+    uint32_t width = 0, height = 0, bandRows = 1;
+    float4* stage = nullptr;          // device 0: the received rows of every device, concatenated
+    float4* full = nullptr;           // device 0: the assembled image, height x width
+    uchar4* ldr = nullptr;            // device 0: tonemap staging
+    bool gathered = false;            // `full` holds the current accumulation
+    std::string err;
+};
+
+static int gfail(pt_group* g, int code, const std::string& msg)
+{
+    if (g) g->err = msg;
+    return code;
+}
+
+#define PT_NCCL_CHECK(g, expr)                                                                   \
+    do {                                                                                         \
+        ncclResult_t r_ = (expr);                                                                \
+        if (r_ != ncclSuccess)                                                                   \
+            return gfail((g), PT_ERR_HIP, std::string("RCCL error ") + ncclGetErrorString(r_) + \
+                                              " at '" #expr "'");                                \
+    } while (0)
+
+#define PT_GHIP_CHECK(g, expr)                                                                   \
+    do {                                                                                         \
+        hipError_t e_ = (expr);                                                                  \
+        if (e_ != hipSuccess)                                                                    \
+            return gfail((g), PT_ERR_HIP, std::string("HIP error ") + hipGetErrorString(e_) +    \
+                                              " at '" #expr "'");                                \
+    } while (0)
+
+// first failing context's status, with its message
+static int gctx_rc(pt_group* g, const std::vector<int>& rc)
+{
+    for (size_t i = 0; i < rc.size(); ++i)
+        if (rc[i] != PT_OK) return gfail(g, rc[i], "device " + std::to_string(g->devices[i]) + ": " + g->ctx[i]->err);
+    return PT_OK;
+}
+
+extern "C" {
+
+PT_API void pt_group_destroy(pt_group* g)
+{
+    if (!g) return;
+    for (ncclComm_t c : g->comms)
+        if (c) (void)ncclCommDestroy(c);
+    if (!g->devices.empty()) (void)hipSetDevice(g->devices[0]);
+    (void)hipFree(g->stage);
+    (void)hipFree(g->full);
+    (void)hipFree(g->ldr);
+    for (pt_context* c : g->ctx) pt_destroy(c);
+    delete g;
+}
+
+PT_API int pt_group_create(int ndev, const int* devices, uint32_t width, uint32_t height, uint32_t band_rows,
+                           pt_group** out)
+{
+    if (!out || ndev < 1 || !devices) return PT_ERR_ARG;
+    *out = nullptr;
+    pt_group* g = new pt_group();
+    g->devices.assign(devices, devices + ndev);
+    g->width = width;
+    g->height = height;
+    g->bandRows = band_rows;
+    auto bail = [&](int rc) { pt_group_destroy(g); return rc; };
+    for (int i = 0; i < ndev; ++i)
+        for (int j = 0; j < i; ++j)
+            if (devices[i] == devices[j]) return bail(PT_ERR_ARG);      // one rank per device (RCCL)
+    size_t staged = 0;
+    for (int i = 0; i < ndev; ++i) {
+        pt_context* c = nullptr;
+        const int rc = pt_create_banded(devices[i], width, height, band_rows, (uint32_t)i, (uint32_t)ndev, &c);
+        if (rc != PT_OK) return bail(rc);
+        g->ctx.push_back(c);
+        g->stageOff.push_back(staged);
+        staged += (size_t)c->rows * width;
+    }
+    g->comms.assign(ndev, nullptr);
+    if (ncclCommInitAll(g->comms.data(), ndev, devices) != ncclSuccess) {
+        g->comms.clear();
+        return bail(PT_ERR_HIP);
+    }
+    if (hipSetDevice(devices[0]) != hipSuccess) return bail(PT_ERR_HIP);
+    if (hipMalloc(&g->stage, std::max<size_t>(staged, 1) * sizeof(float4)) != hipSuccess) return bail(PT_ERR_HIP);
+    if (hipMalloc(&g->full, (size_t)width * height * sizeof(float4)) != hipSuccess) return bail(PT_ERR_HIP);
+    *out = g;
+    return PT_OK;
+}
+
+PT_API int pt_group_size(const pt_group* g) { return g ? (int)g->ctx.size() : 0; }
+
+PT_API pt_context* pt_group_context(pt_group* g, int index)
+{
+    return (g && index >= 0 && index < (int)g->ctx.size()) ? g->ctx[index] : nullptr;
+}
+
+PT_API int pt_group_set_scene(pt_group* g, const pt_bvh_node* nodes, uint32_t node_count, const pt_hittable* prims,
+                              uint32_t prim_count)
+{
+    if (!g) return PT_ERR_ARG;
+    std::vector<int> rc;
+    for (pt_context* c : g->ctx) rc.push_back(pt_set_scene(c, nodes, node_count, prims, prim_count));
+    return gctx_rc(g, rc);
+}
+
+PT_API int pt_group_set_texture(pt_group* g, uint32_t handle, const float* rgba, uint32_t width, uint32_t height)
+{
+    if (!g) return PT_ERR_ARG;
+    std::vector<int> rc;
+    for (pt_context* c : g->ctx) rc.push_back(pt_set_texture(c, handle, rgba, width, height));
+    return gctx_rc(g, rc);
+}
+
+PT_API int pt_group_set_skybox(pt_group* g, uint32_t handle)
+{
+    if (!g) return PT_ERR_ARG;
+    std::vector<int> rc;
+    for (pt_context* c : g->ctx) rc.push_back(pt_set_skybox(c, handle));
+    return gctx_rc(g, rc);
+}
+
+PT_API int pt_group_render(pt_group* g, const pt_camera* camera, uint32_t spp, uint32_t chunks, int ignore_history,
+                           float* gpu_ms)
+{
+    if (!g || !camera) return PT_ERR_ARG;
+    const size_t n = g->ctx.size();
+    std::vector<int> rc(n, PT_OK);
+    std::vector<float> ms(n, 0.0f);
+    auto one = [&](size_t i) { rc[i] = pt_render(g->ctx[i], camera, spp, chunks, ignore_history, &ms[i]); };
+    if (n == 1) {
+        one(0);
+    } else {                                   // one host thread per device: the launches overlap
+        std::vector<std::thread> th;
+        for (size_t i = 0; i < n; ++i) th.emplace_back(one, i);
+        for (auto& t : th) t.join();
+    }
+    g->gathered = false;
+    if (gpu_ms) *gpu_ms = *std::max_element(ms.begin(), ms.end());
+    return gctx_rc(g, rc);
+}
+
+PT_API int pt_group_gather(pt_group* g, float* host_ms)
+{
+    if (!g) return PT_ERR_ARG;
+    const auto t0 = std::chrono::steady_clock::now();
+    const size_t n = g->ctx.size();
+    pt_context* root = g->ctx[0];
+    // every context's stream is idle (pt_render is synchronous); one RCCL group: device i sends
+    // its rows (rows_i x width float4, contiguous) to device 0, which receives them into `stage`
+    PT_NCCL_CHECK(g, ncclGroupStart());
+    for (size_t i = 0; i < n; ++i) {
+        const size_t count = (size_t)g->ctx[i]->rows * g->width * 4;
+        if (count == 0) continue;
+        PT_NCCL_CHECK(g, ncclSend(g->ctx[i]->accum, count, ncclFloat, 0, g->comms[i], g->ctx[i]->stream));
+        PT_NCCL_CHECK(g, ncclRecv(g->stage + g->stageOff[i], count, ncclFloat, (int)i, g->comms[0], root->stream));
+    }
+    PT_NCCL_CHECK(g, ncclGroupEnd());
+    PT_GHIP_CHECK(g, hipSetDevice(root->device));
+    for (size_t i = 0; i < n; ++i) {
+        const size_t npix = (size_t)g->ctx[i]->rows * g->width;
+        if (npix == 0) continue;
+        unpermute_rows_kernel<<<(unsigned)((npix + 255) / 256), 256, 0, root->stream>>>(
+            g->full, g->stage + g->stageOff[i], g->width, g->ctx[i]->rows, (uint32_t)i, (uint32_t)n, root->bandShift);
+        PT_GHIP_CHECK(g, hipGetLastError());
+    }
+    for (size_t i = 0; i < n; ++i) {
+        PT_GHIP_CHECK(g, hipSetDevice(g->ctx[i]->device));
+        PT_GHIP_CHECK(g, hipStreamSynchronize(g->ctx[i]->stream));
+    }
+    g->gathered = true;
+    if (host_ms) *host_ms = std::chrono::duration<float, std::milli>(std::chrono::steady_clock::now() - t0).count();
+    return PT_OK;
+}
+
+PT_API int pt_group_read_accum(pt_group* g, float* dst)
+{
+    if (!g || !dst) return PT_ERR_ARG;
+    if (!g->gathered) {
+        const int rc = pt_group_gather(g, nullptr);
+        if (rc != PT_OK) return rc;
+    }
+    PT_GHIP_CHECK(g, hipSetDevice(g->devices[0]));
+    PT_GHIP_CHECK(g, hipMemcpy(dst, g->full, (size_t)g->width * g->height * sizeof(float4), hipMemcpyDeviceToHost));
+    return PT_OK;
+}
+
+PT_API int pt_group_tonemap(pt_group* g, uint32_t frames, uint8_t* dst)
+{
+    if (!g || !dst) return PT_ERR_ARG;
+    if (!g->gathered) {
+        const int rc = pt_group_gather(g, nullptr);
+        if (rc != PT_OK) return rc;
+    }
+    pt_context* root = g->ctx[0];
+    const size_t npix = (size_t)g->width * g->height;
+    PT_GHIP_CHECK(g, hipSetDevice(root->device));
+    if (!g->ldr) PT_GHIP_CHECK(g, hipMalloc(&g->ldr, npix * sizeof(uchar4)));
+    tonemap_kernel<<<(unsigned)((npix + 255) / 256), 256, 0, root->stream>>>(g->ldr, g->full, npix, frames);
+    PT_GHIP_CHECK(g, hipGetLastError());
+    PT_GHIP_CHECK(g, hipMemcpyAsync(dst, g->ldr, npix * sizeof(uchar4), hipMemcpyDeviceToHost, root->stream));
+    PT_GHIP_CHECK(g, hipStreamSynchronize(root->stream));
+    return PT_OK;
+}
+
+PT_API const char* pt_group_last_error(const pt_group* g) { return g ? g->err.c_str() : "null group"; }
 
 } // extern "C"

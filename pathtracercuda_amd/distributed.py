@@ -1,27 +1,51 @@
-"""Multi-GPU framebuffer tiling and gather.
+"""Multi-GPU framebuffer tiling and gather across processes (bench.py --gpus N).
 
-Rows are interleaved over the ranks (row y -> rank y mod N) so cheap sky rows and expensive
-ground rows spread evenly; RNG seeds depend only on the global pixel index (initRandState.cu:16),
-so any tiling reproduces the single-GPU image bit for bit.  After rendering, each rank's rows are
-gathered to rank 0 with one collective (RCCL over xGMI with the "nccl" backend, or gloo on CPU)
-and un-interleaved there.  No other data-path communication exists.
+The image is cut into bands of `band_rows` rows and band b goes to rank b mod N, so cheap sky
+bands and expensive ground bands spread evenly over the ranks, and with band_rows = 8 every 8x8
+tile a rank renders is a spatially coherent 8x8 tile of the image (with band_rows = 1 -- plain row
+interleaving -- a rank's 8x8 tile spans 8N image rows and its primary rays lose their coherence).
+RNG seeds depend only on the global pixel index (initRandState.cu:16), so every tiling reproduces
+the single-GPU image bit for bit.  After rendering, each rank's rows are gathered to rank 0 with one
+collective (RCCL over xGMI with the "nccl" backend, or gloo on CPU) and scattered into the image
+there.  No other data-path communication exists.  The same partition runs in one process over
+several devices in the native layer (pt_group_*, include/pt_hip.h).
 """
 from __future__ import annotations
 
-
-def rows_of(height: int, rank: int, world: int) -> int:
-    return (height - rank + world - 1) // world if rank < height else 0
+DEFAULT_BAND_ROWS = 8
 
 
-def max_rows(height: int, world: int) -> int:
-    return (height + world - 1) // world
+def rows_of(height: int, rank: int, world: int, band_rows: int = 1) -> int:
+    """Local rows of `rank` (= pt_band_rows of the native layer)."""
+    rows = 0
+    b = rank
+    while b * band_rows < height:
+        rows += min(band_rows, height - b * band_rows)
+        b += world
+    return rows
 
 
-def gather_framebuffer(local, height: int, rank: int, world: int, recv=None, full=None):
-    """Gather the (max_rows, W, 4) per-rank buffers to rank 0 and un-interleave into (H, W, 4).
+def max_rows(height: int, world: int, band_rows: int = 1) -> int:
+    return max(rows_of(height, r, world, band_rows) for r in range(world))
 
-    `local` holds this rank's rows in its first rows_of(height, rank, world) rows.  Returns the
-    full image on rank 0 (None elsewhere).  `recv` / `full` may be preallocated.
+
+def global_rows(height: int, rank: int, world: int, band_rows: int = 1):
+    """Image row of each local row of `rank`, in local order."""
+    out = []
+    b = rank
+    while b * band_rows < height:
+        out.extend(range(b * band_rows, min((b + 1) * band_rows, height)))
+        b += world
+    return out
+
+
+def gather_framebuffer(local, height: int, rank: int, world: int, recv=None, full=None, band_rows: int = 1,
+                       index=None):
+    """Gather the (max_rows, W, 4) per-rank buffers to rank 0 and scatter them into (H, W, 4).
+
+    `local` holds this rank's rows in its first rows_of(height, rank, world, band_rows) rows.
+    Returns the full image on rank 0 (None elsewhere).  `recv`, `full` and `index` (per-rank
+    LongTensors of global_rows on local's device) may be preallocated.
     """
     import torch
     import torch.distributed as dist
@@ -33,7 +57,9 @@ def gather_framebuffer(local, height: int, rank: int, world: int, recv=None, ful
         if full is None:
             full = torch.empty((height,) + tuple(local.shape[1:]), dtype=local.dtype, device=local.device)
         for r in range(world):
-            full[r::world] = recv[r][: rows_of(height, r, world)]
+            idx = index[r] if index is not None else torch.tensor(global_rows(height, r, world, band_rows),
+                                                                  dtype=torch.long, device=local.device)
+            full.index_copy_(0, idx, recv[r][: idx.numel()])
         return full
     dist.gather(local, None, dst=0)
     return None

@@ -30,9 +30,15 @@ def test_no_gpu_calls_fail_cleanly():
         pa.Pathtracer(8, 8)
 
 
-def test_hip_library_is_gfx950(root):
+def test_hip_library_is_gfx950(tmp_path):
+    # llvm-objdump --offloading extracts the device bundles next to its input: run it on a copy in
+    # a temporary directory so nothing lands in the package's lib/
+    import shutil
     import subprocess
-    out = subprocess.run(["/opt/rocm/lib/llvm/bin/llvm-objdump", "--offloading", str(N.HIP_LIB)],
-                         capture_output=True, text=True, cwd="/tmp")
+    lib = tmp_path / N.HIP_LIB.name
+    shutil.copy(N.HIP_LIB, lib)
+    out = subprocess.run(["/opt/rocm/lib/llvm/bin/llvm-objdump", "--offloading", str(lib)],
+                         capture_output=True, text=True, cwd=tmp_path)
     text = out.stdout + out.stderr
     assert "gfx950" in text
+    assert not list(N.HIP_LIB.parent.glob(N.HIP_LIB.name + ".*")), "bundle files in the package lib/"

@@ -167,3 +167,15 @@ def test_white_furnace_bounded(scenes, tmp_path):
     centre = lin[6:10, 6:10].mean()
     assert abs(centre - a) < 0.03          # one bounce into a convex sphere, then the sky (=1)
     assert lin.max() <= bound + 1e-3
+
+
+def test_fast_timing_build_is_bit_identical(scenes):
+    # bench.py's CPU baseline times liboracle_fast.so (-O3 -march=x86-64-v3, contraction off): it
+    # must compute the checker's bits, with any thread count (rows are handed out dynamically)
+    sc = po.load_scene(scenes / "test_shapes.scene.json", 40, 24)
+    a = po.OracleRenderer(sc, 40, 24, threads=1)
+    a.render(sc.camera, 4, True, chunks=2)
+    b = po.OracleRenderer(sc, 40, 24, threads=5, fast=True)
+    b.render(sc.camera, 4, True, chunks=2)
+    assert np.array_equal(a.accum.view(np.uint32), b.accum.view(np.uint32))
+    assert np.array_equal(a.rng_array(), b.rng_array())

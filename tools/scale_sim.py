@@ -1,7 +1,10 @@
-"""Single-GPU estimate of strong-scaling efficiency: renders one rank's share of the bench image
-(rows y = r + k*N, exactly what rank r renders in `bench.py --gpus N`) and compares its time with
-1/N of the full-frame time.  Usage on the GPU box:
-    python tools/scale_sim.py [--ns 1,2,4,8] [--spp 1024]
+"""Single-GPU projection of multi-GPU strong scaling: renders every rank's exact share of the image
+(the tile `bench.py --gpus N` gives rank r) on one MI355X, one after another, and compares the
+slowest rank's kernel time with 1/N of the full-image time.  Two partitions side by side:
+  rows   band_rows = 1: row y -> rank y mod N (round 1's partition)
+  bands  band_rows = 8: 8-row band b -> rank b mod N (the default since round 2)
+The RCCL gather (~0.1 ms for a C4 frame) is not included.  Usage on the GPU box:
+    python tools/scale_sim.py [--width 3840 --height 2160 --spp 4096] [--ns 2,4,8]
 """
 import argparse
 import json
@@ -13,30 +16,37 @@ sys.path.insert(0, str(ROOT))
 import pathtracercuda_amd as pa  # noqa: E402
 
 
-def run(W, H, off, stride, spp, scene, schedule):
-    pt = pa.Pathtracer(W, H, row_offset=off, row_stride=stride)
-    pt.set_schedule(schedule)
+def run(W, H, off, stride, band, spp, scene):
+    pt = pa.Pathtracer(W, H, row_offset=off, row_stride=stride, band_rows=band)
     cam = pt.load_scene(scene)
-    pt.render_raw(cam, 8, 1, True)                       # records tile costs -> sorted order
-    ms = [pt.render_raw(cam, 8, spp // 8, True) for _ in range(2)]
-    return min(ms)
+    pt.render_raw(cam, 8, 1, True)                       # records the tile costs -> sorted order
+    ms = pt.render_raw(cam, 8, spp // 8, True)
+    pt.close()
+    return ms
 
 
 def main():
     ap = argparse.ArgumentParser()
-    ap.add_argument("--ns", default="1,2,4,8")
-    ap.add_argument("--spp", type=int, default=1024)
-    ap.add_argument("--width", type=int, default=1920)
-    ap.add_argument("--height", type=int, default=1080)
+    ap.add_argument("--ns", default="2,4,8")
+    ap.add_argument("--spp", type=int, default=4096)
+    ap.add_argument("--width", type=int, default=3840)
+    ap.add_argument("--height", type=int, default=2160)
     ap.add_argument("--scene", default=str(ROOT / "scenes/generated_scene.scene.json"))
-    ap.add_argument("--schedule", type=int, default=0, help="pt_set_schedule mode (0 sorted tiles, 2 scattered)")
+    ap.add_argument("--partitions", default="rows:1,bands:8")
     a = ap.parse_args()
-    full = run(a.width, a.height, 0, 1, a.spp, a.scene, a.schedule)
-    out = {"schedule": a.schedule, "full_ms": round(full, 2), "per_n": {}}
-    for n in [int(x) for x in a.ns.split(",")]:
-        worst = max(run(a.width, a.height, r, n, a.spp, a.scene, a.schedule) for r in ([0, n - 1] if n > 1 else [0]))
-        out["per_n"][n] = {"rank_ms_max": round(worst, 2), "ideal_ms": round(full / n, 2),
-                           "efficiency": round(full / n / worst, 3)}
+    full = run(a.width, a.height, 0, 1, 1, a.spp, a.scene)
+    out = {"image": f"{a.width}x{a.height}", "spp": a.spp, "full_ms": round(full, 2), "partitions": {}}
+    for part in a.partitions.split(","):
+        name, band = part.split(":")
+        res = {}
+        for n in [int(x) for x in a.ns.split(",")]:
+            ranks = [run(a.width, a.height, r, n, int(band), a.spp, a.scene) for r in range(n)]
+            worst = max(ranks)
+            res[n] = {"rank_ms": [round(x, 2) for x in ranks], "rank_ms_max": round(worst, 2),
+                      "ideal_ms": round(full / n, 2), "efficiency": round(full / n / worst, 3),
+                      "speedup": round(full / worst, 2)}
+            print(json.dumps({name: {n: res[n]}}), flush=True)
+        out["partitions"][name] = {"band_rows": int(band), "per_n": res}
     print(json.dumps(out))
 
 
