@@ -3,6 +3,7 @@
 #   pathtracercuda_amd/lib/libpt_host.so  host C++ layer + C ABI (include/pathtracer_amd.hpp, pt_host.h)
 #   pathtracercuda_amd/lib/pathtracer     CLI (reference main.cpp headless path)
 #   pathtracercuda_amd/lib/fp_exhaustive  all-inputs check of the kernel's fast 1/x and sqrt (GPU)
+#   pathtracercuda_amd/lib/host_sanitize_check  ASan/UBSan mutation check of the host parsers (CPU)
 #   oracle/liboracle.so                   CPU restatement (test infrastructure only)
 # Every FP unit is built with -ffp-contract=off: the GPU result is compared bit for bit with the
 # oracle, and the host-built BVH / transforms / camera feed the GPU directly.
@@ -21,7 +22,7 @@ HIPFLAGS ?= --offload-arch=$(ARCH) -O3 -std=c++17 -ffp-contract=off -fPIC -fvisi
 CXXFLAGS ?= -O2 -std=c++17 -ffp-contract=off -fno-fast-math -fPIC -Iinclude -I$(SRC)/host -Wall -Wextra \
             -Wno-unused-parameter -Wno-missing-field-initializers
 
-all: $(LIB)/libpt_hip.so $(LIB)/libpt_host.so $(LIB)/pathtracer $(LIB)/fp_exhaustive oracle
+all: $(LIB)/libpt_hip.so $(LIB)/libpt_host.so $(LIB)/pathtracer $(LIB)/fp_exhaustive $(LIB)/host_sanitize_check oracle
 
 $(LIB):
 	mkdir -p $(LIB)
@@ -41,8 +42,17 @@ $(LIB)/fp_exhaustive: tools/fp_exhaustive.hip $(SRC)/pt_math.h | $(LIB)
 oracle:
 	$(MAKE) -C oracle
 
+# CPU-only sanitizer build of the host parsers (scene JSON, RGBE/PNG decode, BVH build) with a
+# mutation driver; run by tests/test_host.py.  Links libpt_hip.so for the symbols only (no GPU call).
+SAN_SRCS := $(filter-out $(SRC)/host/host_capi.cpp,$(HOST_SRCS))
+$(LIB)/host_sanitize_check: tools/host_sanitize_check.cpp $(SAN_SRCS) $(HOST_HDRS) $(LIB)/libpt_hip.so
+	$(CXX) -O1 -g -std=c++17 -ffp-contract=off -fsanitize=address,undefined -fno-sanitize-recover=undefined \
+	  -fno-omit-frame-pointer -Iinclude -I$(SRC)/host -o $@ tools/host_sanitize_check.cpp $(SAN_SRCS) \
+	  -L$(LIB) -lpt_hip -lz -lpthread -Wl,-rpath,'$$ORIGIN'
+sanitize: $(LIB)/host_sanitize_check
+
 clean:
 	rm -f $(LIB)/libpt_hip.so $(LIB)/libpt_host.so $(LIB)/pathtracer
 	$(MAKE) -C oracle clean
 
-.PHONY: all oracle clean
+.PHONY: all oracle clean sanitize

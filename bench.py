@@ -136,9 +136,12 @@ def cpu_baseline(args, cfg, W, H):
     from oracle import pyoracle as po
     affinity = len(os.sched_getaffinity(0))
     model, quota = cpu_info()
-    threads = args.cpu_threads or affinity
+    # every core this process may use: the affinity mask, capped by the cgroup's CPU quota (on the
+    # GPU hosts 256 logical CPUs are visible but the job's cgroup grants 16 -- more threads than
+    # that only time-slice the same 16 CPUs; measured 36 Msamples/s at 256 threads vs ~50 at 16)
+    threads = args.cpu_threads or (min(affinity, max(1, int(math.ceil(quota)))) if quota else affinity)
     sc = po.load_scene(scene_path(cfg["scene"]), W, H)
-    pilot = po.OracleRenderer(sc, W, H, 0, max(1, H // 64), threads=threads, fast=True)
+    pilot = po.OracleRenderer(sc, W, H, 0, max(1, H // (4 * threads)), threads=threads, fast=True)
     t0 = time.perf_counter()
     pilot.render(sc.camera, CHUNK, True, chunks=1)
     rate = pilot.rows * W * CHUNK / max(time.perf_counter() - t0, 1e-6)
@@ -151,7 +154,8 @@ def cpu_baseline(args, cfg, W, H):
     return {"value": round(samples / dt / 1e6, 3), "unit": "Msamples/s", "cores": threads, "kind": "port",
             "sample": f"{cfg['scene']} {W}x{H} x {CHUNK * chunks} spp (of {cfg['spp']}) = {samples} samples, "
                       f"{dt:.1f} s on {threads} threads",
-            "cpu_model": model, "affinity_cpus": affinity, "cgroup_cpu_limit": quota,
+            "per_core": round(samples / dt / 1e6 / threads, 3),
+            "cpu_model": model, "host_logical_cpus": os.cpu_count(), "affinity_cpus": affinity, "cgroup_cpu_limit": quota,
             "build": "oracle/liboracle_fast.so: gcc -O3 -march=x86-64-v3 -ffp-contract=off (bit-identical to the checker)"}
 
 

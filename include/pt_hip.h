@@ -172,6 +172,10 @@ PT_API int pt_write_rng(pt_context *ctx, const uint32_t *src);
 
 PT_API uint32_t pt_local_rows(const pt_context *ctx);
 
+/* Shader-clock cycles each 8x8 tile took in the last launch (row-major over the context's tiles,
+ * count = ceil(width / 8) * ceil(rows / 8)); the input of the cost order. */
+PT_API int pt_read_tile_costs(pt_context *ctx, uint32_t *dst, uint32_t count);
+
 /* Tuning knob for A/B measurements: 0 = automatic (default); otherwise one of the shipped
  * trace-kernel variants 1, 4, 6, 20, 40, 41, 46 (traversal loop shape, BVH staged in LDS or read
  * through the caches, occupancy target; see pt_kernels.hip).  All variants produce bit-identical

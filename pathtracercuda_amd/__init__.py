@@ -256,6 +256,13 @@ class Pathtracer:
         """0 = cost-sorted tile dispatch (default), 1 = row-major (pt_set_schedule)."""
         N.check_ctx(N.hip().pt_set_schedule(self._ctx, int(mode)), self._ctx)
 
+    def tile_costs(self) -> np.ndarray:
+        """Shader-clock cycles of each 8x8 tile in the last launch (tiles_y x tiles_x)."""
+        tx, ty = (self.width + 7) // 8, (self.rows + 7) // 8
+        out = np.zeros(tx * ty, dtype=np.uint32)
+        N.check_ctx(N.hip().pt_read_tile_costs(self._ctx, out.ctypes.data_as(C.POINTER(C.c_uint32)), tx * ty), self._ctx)
+        return out.reshape(ty, tx)
+
     def copy_accum_to_device(self, dst_ptr: int, nbytes: int) -> None:
         N.check_ctx(N.hip().pt_copy_accum_device(self._ctx, C.c_void_p(int(dst_ptr)), int(nbytes)), self._ctx)
 

@@ -39,6 +39,12 @@ using namespace pt;
 
 namespace {
 
+// The kernel's dynamic LDS (layout: trace_kernel).  Declared here so device functions address it
+// directly (ds_* instructions; a generic pointer kept in a struct would compile to flat_*).
+extern __shared__ float4 lds4[];
+
+__device__ __forceinline__ float* lds_f() { return reinterpret_cast<float*>(lds4); }
+
 struct DevTex {
     const float4* texels;
     uint32_t width, height;
@@ -58,6 +64,8 @@ struct TraceParams {
     const DevTex* textures;     // 64 entries
     unsigned long long* stats;  // 6 counters (instrumented variant only)
     uint32_t skybox;
+    DevTex skyTex;              // the skybox's descriptor itself (kernel argument: scalar loads, no
+                                // dependent fetch from the texture table per miss)
     uint32_t width, height, rowOffset, rowStride, rows;
     uint32_t bandShift;         // rows are tiled in bands of 1 << bandShift rows (global_row)
     uint32_t spp, chunks, ignoreFirst;
@@ -818,7 +826,8 @@ struct PathState {
     f3 o, d;          // current ray
     f3 L, T;          // radiance and throughput of the current path (trace.cu:104-105)
     f3 color;         // sum of the finished paths of the current render() call (trace.cu:186)
-    float* acc;       // this lane's running accumulation value in LDS (x, y, z at acc[0], [64], [128])
+    uint32_t acc;     // float index of this lane's running accumulation value in the dynamic LDS
+                      // (x, y, z at lds_f()[acc], [acc + 64], [acc + 128])
     uint32_t s, c, bounce;
     bool alive;
 };
@@ -846,7 +855,7 @@ PT_DEV bool shade(const TraceParams& P, const float4* __restrict__ prims, uint32
             const float phi = atan2_sel(ps.d.z, ps.d.x);
             const float v = div_pi(theta);
             const float u = div_two_pi(phi);
-            sky = tex2d(P.textures[P.skybox - 1], u, v);
+            sky = tex2d(P.skyTex, u, v);
         }
         ps.L = add(ps.L, mul(ps.T, sky));
         return true;
@@ -958,10 +967,11 @@ PT_DEV void finish_path(const TraceParams& P, PathState& ps, Xorwow& rng, float 
     if (++ps.s == P.spp) {
         const bool ignore = (ps.c == 0) && P.ignoreFirst;
         f3 acc = ps.color;
-        if (!ignore) acc = add(ps.color, mk(ps.acc[0], ps.acc[64], ps.acc[128]));
-        ps.acc[0] = acc.x;
-        ps.acc[64] = acc.y;
-        ps.acc[128] = acc.z;
+        float* a = lds_f() + ps.acc;
+        if (!ignore) acc = add(ps.color, mk(a[0], a[64], a[128]));
+        a[0] = acc.x;
+        a[64] = acc.y;
+        a[128] = acc.z;
         ps.color = splat(0.0f);
         ps.s = 0;
         if (++ps.c == P.chunks) ps.alive = false;
@@ -1036,7 +1046,7 @@ PT_DEV PixelCtx pixel_of(const TraceParams& P, uint32_t tile, uint32_t lane)
     return pc;
 }
 
-PT_DEV void load_pixel(const TraceParams& P, const PixelCtx& pc, Xorwow& rng, PathState& ps, float* accL)
+PT_DEV void load_pixel(const TraceParams& P, const PixelCtx& pc, Xorwow& rng, PathState& ps, uint32_t accL)
 {
     rng.d = P.rng[pc.li];
     rng.v0 = P.rng[pc.npix + pc.li];
@@ -1047,9 +1057,10 @@ PT_DEV void load_pixel(const TraceParams& P, const PixelCtx& pc, Xorwow& rng, Pa
     ps.acc = accL;
     if (!P.ignoreFirst) {                        // the first call of an ignoreHistory launch overwrites it
         const float4 a = P.accum[pc.li];
-        accL[0] = a.x;
-        accL[64] = a.y;
-        accL[128] = a.z;
+        float* l = lds_f() + accL;
+        l[0] = a.x;
+        l[64] = a.y;
+        l[128] = a.z;
     }
     ps.color = splat(0.0f);
     ps.L = splat(0.0f);
@@ -1066,7 +1077,8 @@ PT_DEV void store_pixel(const TraceParams& P, const PixelCtx& pc, const Xorwow& 
     P.rng[3 * pc.npix + pc.li] = rng.v2;
     P.rng[4 * pc.npix + pc.li] = rng.v3;
     P.rng[5 * pc.npix + pc.li] = rng.v4;
-    P.accum[pc.li] = make_float4(ps.acc[0], ps.acc[64], ps.acc[128], 1.0f);   // trace.cu:198, once per launch
+    const float* a = lds_f() + ps.acc;
+    P.accum[pc.li] = make_float4(a[0], a[64], a[128], 1.0f);   // trace.cu:198, once per launch
 }
 
 // ---------------------------------------------------------------------------------------------
@@ -1081,7 +1093,6 @@ PT_DEV void store_pixel(const TraceParams& P, const PixelCtx& pc, const Xorwow& 
 template <bool STATS, int SL, int WPB, int WW, int MINW, bool PERSIST = false>
 __global__ void __launch_bounds__(WPB * 64, MINW) trace_kernel(TraceParams P)
 {
-    extern __shared__ float4 lds4[];
     const uint32_t lane = threadIdx.x & 63u;
     const uint32_t wave = threadIdx.x >> 6;
     const float4* gnodes = WW >= 3 ? P.cnodes : P.nodes;
@@ -1100,7 +1111,7 @@ __global__ void __launch_bounds__(WPB * 64, MINW) trace_kernel(TraceParams P)
     uint32_t* ldsStacks = reinterpret_cast<uint32_t*>(lds4 + sceneF4);
     const uint32_t stackWords = (WW >= 3 ? 2u : 1u) * P.stackDepth * 64u;
     uint32_t* stack = ldsStacks + wave * stackWords + (WW >= 3 ? 2u : 1u) * lane;
-    float* accL = reinterpret_cast<float*>(ldsStacks + WPB * stackWords) + wave * 192u + lane;
+    const uint32_t accL = 4u * sceneF4 + WPB * stackWords + wave * 192u + lane;   // float index
     Counters cnt = {};
     uint32_t slot = PERSIST ? wave_fetch(P.tileCursor, 1u) : blockIdx.x * (uint32_t)WPB + wave;
     for (;;) {
@@ -1660,6 +1671,7 @@ static int render_impl(pt_context* ctx, const pt_camera* cam, uint32_t spp, uint
     P.textures = ctx->texTable;
     P.stats = ctx->stats;
     P.skybox = ctx->skybox;
+    if (ctx->skybox != 0) P.skyTex = ctx->hostTex[ctx->skybox - 1];
     P.width = ctx->width;
     P.height = ctx->height;
     P.rowOffset = ctx->rowOffset;
@@ -1892,6 +1904,16 @@ PT_API int pt_write_rng(pt_context* ctx, const uint32_t* src)
 }
 
 PT_API uint32_t pt_local_rows(const pt_context* ctx) { return ctx ? ctx->rows : 0; }
+
+PT_API int pt_read_tile_costs(pt_context* ctx, uint32_t* dst, uint32_t count)
+{
+    if (!ctx || !dst) return PT_ERR_ARG;
+    if (!ctx->tileCost || count != ctx->orderTiles) return fail(ctx, PT_ERR_STATE, "pt_read_tile_costs: no costs of that size");
+    PT_HIP_CHECK(ctx, hipSetDevice(ctx->device));
+    PT_HIP_CHECK(ctx, hipStreamSynchronize(ctx->stream));
+    PT_HIP_CHECK(ctx, hipMemcpy(dst, ctx->tileCost, (size_t)count * sizeof(uint32_t), hipMemcpyDeviceToHost));
+    return PT_OK;
+}
 
 PT_API int pt_set_kernel_variant(pt_context* ctx, int variant)
 {

@@ -1,5 +1,6 @@
 """Host C++ layer (libpt_host.so) without a GPU: scene loading, transforms, SAH BVH, camera and
 image I/O, checked against the independent oracle restatement and the reference's semantics."""
+import os
 import ctypes as C
 import json
 
@@ -241,3 +242,21 @@ def test_parallel_bvh_build_identical_to_sequential(tmp_path, root, monkeypatch)
     assert seq.object_count == par.object_count > 10000
     assert bytes(n1) == bytes(n8) and bytes(p1) == bytes(p8)
     assert par.timing()["bvh_ms"] > 0.0
+
+
+def test_host_parsers_under_asan_ubsan(tmp_path, root, scenes):
+    # the scene JSON reader (json_min.cpp / scene_json.cpp) and the RGBE/PNG decoder
+    # (image_io.cpp) read untrusted files (SceneLoader.cpp:199-219, Pathtracer.cpp:245-251).  The
+    # sanitizer build (make sanitize) parses every committed scene and texture plus ~8,000
+    # truncated / byte-flipped / structurally edited variants, builds BVHs of the scenes that parse
+    # and writes the images back: any ASan or UBSan report fails the run.
+    import subprocess
+    exe = root / "pathtracercuda_amd" / "lib" / "host_sanitize_check"
+    files = [scenes / f for f in ("cornell_box.scene.json", "test_shapes.scene.json", "generated_scene.scene.json",
+                                  "checker.png", "skybox.hdr")]
+    env = dict(os.environ, ASAN_OPTIONS="detect_leaks=1:abort_on_error=1", UBSAN_OPTIONS="print_stacktrace=1")
+    r = subprocess.run([str(exe), str(tmp_path)] + [str(f) for f in files], capture_output=True, text=True, errors="replace",
+                       timeout=600, env=env)
+    assert r.returncode == 0, r.stderr[-4000:]
+    assert "no sanitizer report" in r.stdout
+    assert "ERROR: AddressSanitizer" not in r.stderr and "runtime error" not in r.stderr
