@@ -22,6 +22,7 @@ ap.add_argument("--rank", type=int, default=0)
 ap.add_argument("--band", type=int, default=8)
 ap.add_argument("--reps", type=int, default=2)
 ap.add_argument("--scene", default=str(ROOT / "scenes/generated_scene.scene.json"))
+ap.add_argument("--save", default="", help="write the last run's tile-cost map (.npy)")
 a = ap.parse_args()
 pt = pa.Pathtracer(a.width, a.height, row_offset=a.rank, row_stride=a.n, band_rows=a.band)
 cam = pt.load_scene(a.scene)
@@ -37,4 +38,6 @@ for rep in range(a.reps):
         out["runs"].setdefault(str(p), []).append({"ms": round(ms, 2), "tile_Mcycles_p50_p90_p99_p999_max": [round(x / 1e6, 2) for x in q],
                                                    "tile_Mcycles_mean": round(c.mean() / 1e6, 2)})
         print(json.dumps({p: out["runs"][str(p)][-1]}), flush=True)
+if a.save:
+    np.save(a.save, pt.tile_costs())
 print(json.dumps(out))

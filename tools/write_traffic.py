@@ -14,6 +14,7 @@ from pmc_summary import load  # noqa: E402
 def main():
     src = pathlib.Path(sys.argv[1]) if len(sys.argv) > 1 else ROOT / "gpurun_out" / "pmc_bench"
     tag = sys.argv[2] if len(sys.argv) > 2 else "r01"
+    workload = sys.argv[3] if len(sys.argv) > 3 else "generated_scene 1920x1080 1024spp chunk8"
     disp, names = load(src, "trace_kernel<false")
     best = {}
     for (p, i), c in disp.items():
@@ -24,7 +25,7 @@ def main():
         merged.update({k: v for k, v in c.items() if k != "DURATION_NS"})
         merged.setdefault("duration_ns", c.get("DURATION_NS"))
     fetch, write = merged.get("FETCH_SIZE"), merged.get("WRITE_SIZE")
-    out = {"workload": "generated_scene 1920x1080 1024spp chunk8", "kernel": "trace_kernel (timed launch)",
+    out = {"workload": workload, "kernel": "trace_kernel (timed launch)",
            "fetch_size_kib": fetch, "write_size_kib": write,
            "bytes_per_launch": (2 * fetch + write) * 1024 if fetch is not None and write is not None else None,
            "correction": "FETCH_SIZE x2 (gfx950 reports half of wide coalesced reads); KiB -> bytes",
