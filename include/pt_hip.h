@@ -187,6 +187,17 @@ PT_API int pt_set_kernel_variant(pt_context *ctx, int variant);
  * rebuilt on the device from the latest launch), 1 = always row-major.  Results are identical;
  * only the launch tail changes. */
 PT_API int pt_set_schedule(pt_context *ctx, int mode);
+
+/* Speculative sample groups.  A pixel's samples are one serial XORWOW stream
+ * (trace.cu:183-193), so a launch with fewer 8x8 tiles than about four per wave slot of the chip
+ * (multi-GPU strong scaling, small images) lasts as long as its slowest tile's whole chain.  With
+ * groups, each pixel's chain is cut into G pieces started at guessed draw offsets and stitched where
+ * the guessed parse meets the true one; results stay bit-identical.  mode: 0 = automatic (default),
+ * 1 = never, G >= 2 = always G groups (tests).  pt_last_sample_groups: groups of the last launch
+ * (0 = plain); pt_read_resume_count: pixels the last grouped launch finished in its resume pass. */
+PT_API int pt_set_sample_groups(pt_context *ctx, int mode);
+PT_API int pt_last_sample_groups(const pt_context *ctx);
+PT_API int pt_read_resume_count(pt_context *ctx, uint32_t *count);
 PT_API const char *pt_last_error(const pt_context *ctx);
 
 /* ---- Multi-device group (one process, one context per GPU, RCCL over xGMI) -------------------

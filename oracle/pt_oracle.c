@@ -1403,6 +1403,36 @@ OR_EXPORT int or_render(const or_hittable *prims, uint32_t primCount, const or_b
     return err ? -1 : 0;
 }
 
+/* Test infrastructure for the speculative sample groups: the raw draw stream of one
+ * pixel, and its per-sample log from any starting state -- the colour getColor returns
+ * (trace.cu:190-193) and the draw pairs the sample consumed (1 for the jitter + 1 per hit,
+ * Material.inl:40-41).  Same operations as render_rows. */
+OR_EXPORT void or_xorwow_skip(xorwow_t *s, uint64_t draws)
+{
+    while (draws--) (void)xorwow_next(s);
+}
+
+OR_EXPORT int or_sample_log(const or_hittable *prims, uint32_t primCount, const or_bvh_node *nodes, uint32_t nodeCount,
+                            const or_camera *cam, uint32_t skyboxHandle, const or_texture *textures, uint32_t textureCount,
+                            uint32_t width, uint32_t height, uint32_t x, uint32_t y, xorwow_t *state, uint32_t n,
+                            float *colors, uint8_t *pairs)
+{
+    or_scene s = { prims, primCount, nodes, nodeCount, skyboxHandle, textures, textureCount };
+    int err = 0;
+    for (uint32_t i = 0; i < n; ++i) {
+        const uint32_t d0 = state->d;
+        float u = ((float)(int32_t)x + xorwow_uniform(state)) / (float)width;
+        float v = ((float)(int32_t)y + xorwow_uniform(state)) / (float)height;
+        ray_t r;
+        r.o = cam->origin;
+        r.d = v3_normalize(v3_add(v3_add(cam->lowerLeftCorner, v3_scale(u, cam->horizontal)), v3_scale(v, cam->vertical)));
+        v3 c = get_color(&s, r, state, NULL, &err);
+        colors[3 * i] = c.x; colors[3 * i + 1] = c.y; colors[3 * i + 2] = c.z;
+        pairs[i] = (uint8_t)(((state->d - d0) * 0x385e5f0du /* 1/362437 mod 2^32 */) / 2u);
+    }
+    return err ? -1 : 0;
+}
+
 /* tonemap.cu:4-27 (frames = the divisor passed by the caller, Pathtracer.cpp:328) */
 OR_EXPORT void or_tonemap(const float *accum, size_t npix, uint32_t frames, uint8_t *out)
 {

@@ -116,6 +116,11 @@ def _bind(L: C.CDLL) -> C.CDLL:
             getattr(L, name).restype = f
             getattr(L, name).argtypes = [f, f]
         L.or_tex2d.argtypes = [P(Texture), f, f, P(f)]
+        L.or_xorwow_skip.argtypes = [P(Xorwow), C.c_uint64]
+        L.or_sample_log.restype = C.c_int
+        L.or_sample_log.argtypes = [P(Hittable), C.c_uint32, P(BVHNode), C.c_uint32, P(Camera), C.c_uint32, P(Texture),
+                                    C.c_uint32, C.c_uint32, C.c_uint32, C.c_uint32, C.c_uint32, P(Xorwow), C.c_uint32,
+                                    P(f), P(C.c_uint8)]
         L.or_sizeof.restype = C.c_uint32
         L.or_sizeof.argtypes = [C.c_int]
     return L
@@ -402,3 +407,27 @@ class OracleRenderer:
 
 def struct_bytes(arr) -> bytes:
     return bytes(arr)
+
+
+def pixel_state(width: int, x: int, y: int, draws: int = 0) -> Xorwow:
+    """The pixel's XORWOW state (initRandState.cu:16) after `draws` draws."""
+    st = Xorwow()
+    lib().or_xorwow_init(1984 + x + y * width, C.byref(st))
+    if draws:
+        lib().or_xorwow_skip(C.byref(st), draws)
+    return st
+
+
+def sample_log(scene: OracleScene, width: int, height: int, x: int, y: int, state: Xorwow, n: int):
+    """n samples of pixel (x, y) from `state` (advanced in place): per-sample colours (n x 3 float32,
+    what getColor returns) and draw pairs consumed (n uint8)."""
+    cols = np.zeros((n, 3), dtype=np.float32)
+    pairs = np.zeros(n, dtype=np.uint8)
+    tex = scene.texture_table()
+    rc = lib().or_sample_log(scene.prims, scene.prim_count, scene.nodes, scene.node_count, C.byref(scene.camera),
+                             scene.skybox, tex, len(scene.textures), width, height, x, y, C.byref(state), n,
+                             fptr(cols), pairs.ctypes.data_as(C.POINTER(C.c_uint8)))
+    if rc != 0:
+        raise RuntimeError("oracle: BVH traversal stack overflow (reference UB)")
+    return cols, pairs
+

@@ -256,6 +256,20 @@ class Pathtracer:
         """0 = cost-sorted tile dispatch (default), 1 = row-major (pt_set_schedule)."""
         N.check_ctx(N.hip().pt_set_schedule(self._ctx, int(mode)), self._ctx)
 
+    def set_sample_groups(self, mode: int) -> None:
+        """Speculative sample groups (pt_set_sample_groups): 0 = automatic, 1 = off, G >= 2 = always G."""
+        N.check_ctx(N.hip().pt_set_sample_groups(self._ctx, int(mode)), self._ctx)
+
+    @property
+    def last_sample_groups(self) -> int:
+        return int(N.hip().pt_last_sample_groups(self._ctx))
+
+    def resume_count(self) -> int:
+        """Pixels the last grouped launch finished in its resume pass."""
+        n = C.c_uint32(0)
+        N.check_ctx(N.hip().pt_read_resume_count(self._ctx, C.byref(n)), self._ctx)
+        return int(n.value)
+
     def tile_costs(self) -> np.ndarray:
         """Shader-clock cycles of each 8x8 tile in the last launch (tiles_y x tiles_x)."""
         tx, ty = (self.width + 7) // 8, (self.rows + 7) // 8

@@ -80,8 +80,25 @@ struct TraceParams {
     uint32_t numSlots;          // dispatch slots = 8x8 tiles
     uint32_t* tileCost;         // per-tile shader-clock cycles of this launch (null: not recorded)
     uint32_t discard;           // != 0: cost pre-pass -- pixel state (RNG, accum) is read, never written
+    float* pairsOut;            // cost pre-pass: per-pixel draw pairs per sample (speculative groups' guess)
+    // Speculative sample groups (0 = off).  Work item = (tile, group g): slot s runs
+    // tile order[s / ssgG], group s % ssgG; item index = tile * ssgG + g.
+    uint32_t ssgG;              // groups per pixel
+    uint32_t ssgCap;            // sample-log capacity per item
+    uint32_t ssgLastN;          // the last group stops after this many samples
+    float* ssgLog;              // [item][cap][3][64] path colours
+    uint16_t* ssgEnd;           // [item][cap][64] end of each sample, in draw pairs from the item's start
+    const uint32_t* ssgStart;   // [item][7][64] start offset (draw pairs), then the state d, v0..v4
+    unsigned long long* ssgBits;// [item][kWinWords][64] the item's sample starts in its first kWinPairs pairs
+    uint32_t* ssgCount;         // [item][64] samples logged
+    const uint32_t* resume;     // resume launch: [4][rows*width] colour x/y/z bits, s | c << 16 | valid << 31
     DevCamera cam;
 };
+
+// Speculative sample groups: window of a group's start offset in which an earlier group's parse can
+// join it (draw pairs; 8 x 64-bit words per lane).
+constexpr uint32_t kWinWords = 8;
+constexpr uint32_t kWinPairs = 64 * kWinWords;
 
 // Row tiling of an image across contexts (multi-GPU): the image is cut into bands of
 // B = 1 << shift rows, and a context owns bands b = offset + k * stride.  Local row ly lies in the
@@ -1016,6 +1033,111 @@ PT_DEV uint32_t wave_fetch(uint32_t* cursor, uint32_t n)
     return (uint32_t)__shfl((int)base, (int)leader, 64);
 }
 
+// ---------------------------------------------------------------------------------------------
+// Speculative sample groups.  A pixel's samples are one serial XORWOW stream, so
+// a tile costs as long as its slowest pixel's whole chain.  When a launch holds too few tiles to
+// fill the chip (multi-GPU strong scaling, small images), each pixel's chain is cut into G groups:
+// group g >= 1 starts at a guessed draw offset (the pixel's measured draw pairs per sample x g x n)
+// with the XORWOW state of that offset, and logs each sample's colour and end offset.  A sample
+// starts wherever the previous one ended, so two parses of one stream that share a sample start
+// coincide from there on: a group's parse becomes the true one where the true parse reaches one of
+// its sample starts (a junction).  Each item records its sample starts near its own start; an
+// earlier item stops at its first junction with a later one.  ssg_fold_kernel then walks the true
+// parse through the logs, folds colours in the reference's order (trace.cu:186-198) and sets the
+// final state; whatever the logs do not cover runs in a resume launch.  Results are bit-identical.
+// ---------------------------------------------------------------------------------------------
+struct SsgLane {
+    uint32_t item;      // tile * G + g
+    uint32_t g;
+    uint32_t k;         // samples logged
+    uint32_t d0;        // Weyl word at the item's start
+    uint32_t base;      // start offset of the item (draw pairs)
+    uint32_t h;         // next group whose window this parse may reach (G: none)
+    uint32_t hStart;    // its start offset
+    uint32_t limit;     // samples before the item stops regardless
+};
+
+PT_DEV uint32_t ssg_start_word(const TraceParams& P, uint32_t item, uint32_t w, uint32_t lane)
+{
+    return P.ssgStart[((size_t)item * 7 + w) * 64 + lane];
+}
+
+PT_DEV void ssg_load(const TraceParams& P, uint32_t tile, uint32_t g, uint32_t lane, size_t li, size_t npix,
+                     Xorwow& rng, PathState& ps, SsgLane& sl)
+{
+    sl.item = tile * P.ssgG + g;
+    sl.g = g;
+    sl.k = 0;
+    if (g == 0) {
+        rng.d = P.rng[li];
+        rng.v0 = P.rng[npix + li];
+        rng.v1 = P.rng[2 * npix + li];
+        rng.v2 = P.rng[3 * npix + li];
+        rng.v3 = P.rng[4 * npix + li];
+        rng.v4 = P.rng[5 * npix + li];
+        sl.base = 0;
+    } else {
+        sl.base = ssg_start_word(P, sl.item, 0, lane);
+        rng.d = ssg_start_word(P, sl.item, 1, lane);
+        rng.v0 = ssg_start_word(P, sl.item, 2, lane);
+        rng.v1 = ssg_start_word(P, sl.item, 3, lane);
+        rng.v2 = ssg_start_word(P, sl.item, 4, lane);
+        rng.v3 = ssg_start_word(P, sl.item, 5, lane);
+        rng.v4 = ssg_start_word(P, sl.item, 6, lane);
+        // the item's own start is its first sample start
+        __hip_atomic_fetch_or(&P.ssgBits[(size_t)sl.item * kWinWords * 64 + lane], 1ull, __ATOMIC_RELAXED,
+                              __HIP_MEMORY_SCOPE_AGENT);
+    }
+    sl.d0 = rng.d;
+    sl.h = g + 1;
+    sl.hStart = sl.h < P.ssgG ? ssg_start_word(P, sl.item + 1, 0, lane) : 0xffffffffu;
+    sl.limit = g + 1 == P.ssgG ? P.ssgLastN : P.ssgCap;
+    ps.L = splat(0.0f);
+    ps.T = splat(1.0f);
+    ps.bounce = 0;
+    ps.alive = sl.limit > 0;
+}
+
+// End of a path in a speculative group: log it, record the sample start that follows, stop at a
+// junction with a later group (or at the item's limit), else start the next sample.
+template <bool STATS>
+PT_DEV void ssg_finish(const TraceParams& P, PathState& ps, Xorwow& rng, float fx, float fy, SsgLane& sl,
+                       uint32_t lane, Counters& cnt)
+{
+    if (STATS) cnt.samples++;
+    const size_t rec = (size_t)sl.item * P.ssgCap + sl.k;
+    P.ssgLog[(rec * 3 + 0) * 64 + lane] = ps.L.x;
+    P.ssgLog[(rec * 3 + 1) * 64 + lane] = ps.L.y;
+    P.ssgLog[(rec * 3 + 2) * 64 + lane] = ps.L.z;
+    const uint32_t rel = ((rng.d - sl.d0) * kInvWeyl) >> 1;          // draw pairs since the item's start
+    P.ssgEnd[rec * 64 + lane] = (uint16_t)rel;
+    ++sl.k;
+    bool stop = sl.k >= sl.limit;
+    if (sl.g > 0 && rel < kWinPairs)
+        __hip_atomic_fetch_or(&P.ssgBits[((size_t)sl.item * kWinWords + rel / 64) * 64 + lane], 1ull << (rel % 64),
+                              __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    const uint32_t off = sl.base + rel;
+    while (sl.h < P.ssgG && off >= sl.hStart + kWinPairs) {          // passed that group's window
+        ++sl.h;
+        sl.hStart = sl.h < P.ssgG ? ssg_start_word(P, sl.item - sl.g + sl.h, 0, lane) : 0xffffffffu;
+    }
+    if (!stop && sl.h < P.ssgG && off >= sl.hStart) {
+        const uint32_t w = off - sl.hStart;
+        const unsigned long long bits = __hip_atomic_load(
+            &P.ssgBits[((size_t)(sl.item - sl.g + sl.h) * kWinWords + w / 64) * 64 + lane], __ATOMIC_RELAXED,
+            __HIP_MEMORY_SCOPE_AGENT);
+        stop = (bits >> (w % 64)) & 1ull;                              // junction: group h carries on
+    }
+    if (stop) {
+        ps.alive = false;
+        return;
+    }
+    camera_ray(P, fx, fy, rng, ps.o, ps.d);
+    ps.L = splat(0.0f);
+    ps.T = splat(1.0f);
+    ps.bounce = 0;
+}
+
 struct PixelCtx {
     bool valid;
     uint32_t px, py;
@@ -1046,8 +1168,10 @@ PT_DEV PixelCtx pixel_of(const TraceParams& P, uint32_t tile, uint32_t lane)
     return pc;
 }
 
+template <bool AUX>
 PT_DEV void load_pixel(const TraceParams& P, const PixelCtx& pc, Xorwow& rng, PathState& ps, uint32_t accL)
 {
+    // AUX: resume launches (see ssg_fold_kernel; pixels the fold finished are skipped by the caller)
     rng.d = P.rng[pc.li];
     rng.v0 = P.rng[pc.npix + pc.li];
     rng.v1 = P.rng[2 * pc.npix + pc.li];
@@ -1055,7 +1179,7 @@ PT_DEV void load_pixel(const TraceParams& P, const PixelCtx& pc, Xorwow& rng, Pa
     rng.v3 = P.rng[4 * pc.npix + pc.li];
     rng.v4 = P.rng[5 * pc.npix + pc.li];
     ps.acc = accL;
-    if (!P.ignoreFirst) {                        // the first call of an ignoreHistory launch overwrites it
+    if (!P.ignoreFirst || (AUX && P.resume)) {   // the first call of an ignoreHistory launch overwrites it
         const float4 a = P.accum[pc.li];
         float* l = lds_f() + accL;
         l[0] = a.x;
@@ -1067,6 +1191,14 @@ PT_DEV void load_pixel(const TraceParams& P, const PixelCtx& pc, Xorwow& rng, Pa
     ps.T = splat(1.0f);
     ps.s = ps.c = ps.bounce = 0;
     ps.alive = P.chunks > 0 && P.spp > 0;
+    if (AUX && P.resume) {                       // mid-launch state left by ssg_fold_kernel
+        ps.color = mk(__uint_as_float(P.resume[pc.li]), __uint_as_float(P.resume[pc.npix + pc.li]),
+                      __uint_as_float(P.resume[2 * pc.npix + pc.li]));
+        const uint32_t sc = P.resume[3 * pc.npix + pc.li];
+        ps.s = sc & 0xffffu;
+        ps.c = (sc >> 16) & 0x7fffu;
+        ps.alive = ps.c < P.chunks;
+    }
 }
 
 PT_DEV void store_pixel(const TraceParams& P, const PixelCtx& pc, const Xorwow& rng, const PathState& ps)
@@ -1090,9 +1222,14 @@ PT_DEV void store_pixel(const TraceParams& P, const PixelCtx& pc, const Xorwow& 
 // One wave = one 8x8 tile.  PERSIST: the grid holds only the resident waves, and each wave takes
 // the next dispatch slot from a global counter when its tile is done, so a wave never waits for
 // the other waves of its workgroup (which would keep the group's LDS and slots idle).
-template <bool STATS, int SL, int WPB, int WW, int MINW, bool PERSIST = false>
+// MODE 0: plain; 1 (SSG): speculative sample groups (ssg_load / ssg_finish), one work item per
+// (tile, group); 2: auxiliary launches -- the resume pass after a grouped launch, and the cost
+// pre-pass that also measures draw pairs per sample.  Separate instantiations keep the plain
+// kernel's register allocation free of their code.
+template <bool STATS, int SL, int WPB, int WW, int MINW, bool PERSIST = false, int MODE = 0>
 __global__ void __launch_bounds__(WPB * 64, MINW) trace_kernel(TraceParams P)
 {
+    constexpr bool SSG = MODE == 1, AUX = MODE == 2;
     const uint32_t lane = threadIdx.x & 63u;
     const uint32_t wave = threadIdx.x >> 6;
     const float4* gnodes = WW >= 3 ? P.cnodes : P.nodes;
@@ -1116,13 +1253,23 @@ __global__ void __launch_bounds__(WPB * 64, MINW) trace_kernel(TraceParams P)
     uint32_t slot = PERSIST ? wave_fetch(P.tileCursor, 1u) : blockIdx.x * (uint32_t)WPB + wave;
     for (;;) {
     if (PERSIST && slot >= P.numSlots) break;
-    const uint32_t tile = P.order ? P.order[slot] : slot;
+    uint32_t tile, grp = 0;
+    if (SSG) {
+        const uint32_t ts = slot / P.ssgG;
+        grp = slot - ts * P.ssgG;
+        tile = P.order ? P.order[ts] : ts;
+    } else {
+        tile = P.order ? P.order[slot] : slot;
+    }
     const PixelCtx pc = pixel_of(P, tile, lane);
     const uint64_t tWave = __builtin_amdgcn_s_memtime();
-    if (pc.valid) {
+    const bool run = pc.valid && (!AUX || !P.resume || (P.resume[3 * pc.npix + pc.li] >> 31));
+    if (run) {
         Xorwow rng;
         PathState ps;
-        load_pixel(P, pc, rng, ps, accL);
+        SsgLane sl;
+        if (SSG) ssg_load(P, tile, grp, lane, pc.li, pc.npix, rng, ps, sl);
+        else load_pixel<AUX>(P, pc, rng, ps, accL);
         const float fx = (float)(int32_t)pc.px, fy = (float)(int32_t)pc.py;
         camera_ray(P, fx, fy, rng, ps.o, ps.d);
         uint64_t tAll = STATS ? __builtin_amdgcn_s_memtime() : 0;
@@ -1137,7 +1284,10 @@ __global__ void __launch_bounds__(WPB * 64, MINW) trace_kernel(TraceParams P)
                 fresh = tdone;
                 if (!tdone) continue;                              // suspended: resumes next round
                 uint64_t tS = STATS ? __builtin_amdgcn_s_memtime() : 0;
-                if (shade<STATS>(P, prims, ts.elem, ts.tMax, ps, rng, cnt)) finish_path<STATS>(P, ps, rng, fx, fy, cnt);
+                if (shade<STATS>(P, prims, ts.elem, ts.tMax, ps, rng, cnt)) {
+                    if (SSG) ssg_finish<STATS>(P, ps, rng, fx, fy, sl, lane, cnt);
+                    else finish_path<STATS>(P, ps, rng, fx, fy, cnt);
+                }
                 if (STATS) wave_time(cnt.cyc_shade, tS);
                 if (STATS && !ps.alive) tDone = __builtin_amdgcn_s_memtime();
             }
@@ -1148,15 +1298,24 @@ __global__ void __launch_bounds__(WPB * 64, MINW) trace_kernel(TraceParams P)
             const uint32_t e = WW >= 3 ? traverse_cb<STATS>(nodes, prims, reinterpret_cast<uint2*>(stack), P, ps.o, ps.d, t, cnt)
                                        : traverse<STATS, WW>(nodes, prims, stack, ps.o, ps.d, P.slabFast != 0, t, cnt);
             uint64_t tS = STATS ? __builtin_amdgcn_s_memtime() : 0;
-            if (shade<STATS>(P, prims, e, t, ps, rng, cnt)) finish_path<STATS>(P, ps, rng, fx, fy, cnt);
+            if (shade<STATS>(P, prims, e, t, ps, rng, cnt)) {
+                if (SSG) ssg_finish<STATS>(P, ps, rng, fx, fy, sl, lane, cnt);
+                else finish_path<STATS>(P, ps, rng, fx, fy, cnt);
+            }
             if (STATS) wave_time(cnt.cyc_shade, tS);
         }
         if (STATS && WW >= 100 && tDone) cnt.cyc_lane_idle += __builtin_amdgcn_s_memtime() - tDone;
         if (STATS) wave_time(cnt.cyc_total, tAll);
-        if (!P.discard) store_pixel(P, pc, rng, ps);
+        if (SSG) P.ssgCount[(size_t)sl.item * 64 + lane] = sl.k;
+        else if (!P.discard) store_pixel(P, pc, rng, ps);
+        else if (AUX && P.pairsOut)           // cost pre-pass: draw pairs per sample of this pixel
+            P.pairsOut[pc.li] = (float)(((rng.d - P.rng[pc.li]) * kInvWeyl) >> 1) / (float)(P.spp * P.chunks);
     }
-    if (P.tileCost && lane == 0 && tile < P.tilesX * P.tilesY)
-        P.tileCost[tile] = (uint32_t)min(__builtin_amdgcn_s_memtime() - tWave, (uint64_t)0xffffffffu);
+    if (P.tileCost && lane == 0 && tile < P.tilesX * P.tilesY) {
+        const uint32_t cyc = (uint32_t)min(__builtin_amdgcn_s_memtime() - tWave, (uint64_t)0xffffffffu);
+        if (SSG) atomicAdd(&P.tileCost[tile], cyc / P.ssgG);   // zeroed before the launch
+        else P.tileCost[tile] = cyc;
+    }
     if (!PERSIST) break;
     slot = wave_fetch(P.tileCursor, 1u);
     }
@@ -1211,6 +1370,141 @@ __global__ void __launch_bounds__(256) tonemap_kernel(uchar4* out, const float4*
     out[i] = make_uchar4(q[0], q[1], q[2], 255);
 }
 
+// ---- speculative sample groups: start states and the fold ---------------------
+// Both run one lane per pixel, indexed like the trace kernel's items (tile, lane), so the per-item
+// buffers ([item][..][64]) are read and written in whole 256-B rows.
+PT_DEV bool ssg_pixel(const TraceParams& P, size_t gid, uint32_t& tile, uint32_t& lane, size_t& li)
+{
+    tile = (uint32_t)(gid >> 6);
+    lane = (uint32_t)(gid & 63u);
+    const uint32_t tileX = tile % P.tilesX, tileY = tile / P.tilesX;
+    const uint32_t px = tileX * 8u + (lane & 7u), ly = tileY * 8u + (lane >> 3);
+    li = (size_t)ly * P.width + px;
+    return tileY < P.tilesY && px < P.width && ly < P.rows;
+}
+
+// Group g >= 1 of a pixel starts at draw pair round(g * n * m), m = the pixel's draw pairs per
+// sample (the previous launch's, or the cost pre-pass's), strictly increasing in g; its state is
+// the pixel's current state advanced that far.
+__global__ void __launch_bounds__(256) ssg_guess_kernel(TraceParams P, const float* __restrict__ pairs, uint32_t n,
+                                                        uint32_t* __restrict__ start)
+{
+    uint32_t tile, lane;
+    size_t li;
+    if (!ssg_pixel(P, (size_t)blockIdx.x * 256 + threadIdx.x, tile, lane, li)) return;
+    const size_t npix = (size_t)P.rows * P.width;
+    Xorwow st = {P.rng[li], P.rng[npix + li], P.rng[2 * npix + li], P.rng[3 * npix + li], P.rng[4 * npix + li],
+                 P.rng[5 * npix + li]};
+    float m = pairs ? pairs[li] : 2.0f;
+    m = (m >= 1.0f) ? fminf(m, 6.0f) : 1.0f;       // 1..6 pairs per sample (jitter + up to 5 hits)
+    uint32_t off = 0;
+    for (uint32_t g = 1; g < P.ssgG; ++g) {
+        uint32_t o = (uint32_t)((float)(g * n) * m + 0.5f);
+        if (o <= off) o = off + 1;
+        xorwow_skip(st, 2u * (o - off));
+        off = o;
+        uint32_t* w = start + (size_t)(tile * P.ssgG + g) * 7 * 64 + lane;
+        w[0] = o;
+        w[64] = st.d;
+        w[128] = st.v0;
+        w[192] = st.v1;
+        w[256] = st.v2;
+        w[320] = st.v3;
+        w[384] = st.v4;
+    }
+}
+
+// Walk each pixel's true parse through the logs: from group 0, at every sample start check whether a
+// later group's parse has a sample start there (its window bits) and, if that group logged samples
+// from there, continue in its log.  Colours are summed per render() call and folded into the
+// accumulation value exactly as trace.cu:186-198 does; the final XORWOW state is the state at the
+// last consumed sample's end (the item's start state advanced by the draws since).  Pixels whose logs
+// end before spp x chunks samples get a resume record (and a resume launch runs the rest).
+__global__ void __launch_bounds__(256) ssg_fold_kernel(TraceParams P, uint32_t* __restrict__ resume,
+                                                       float* __restrict__ pairs, uint32_t* __restrict__ resumeCount)
+{
+    uint32_t tile, lane;
+    size_t li;
+    if (!ssg_pixel(P, (size_t)blockIdx.x * 256 + threadIdx.x, tile, lane, li)) return;
+    const size_t npix = (size_t)P.rows * P.width;
+    const uint32_t G = P.ssgG, item0 = tile * G, total = P.spp * P.chunks;
+    f3 acc = splat(0.0f);
+    if (!P.ignoreFirst) {
+        const float4 a = P.accum[li];
+        acc = mk(a.x, a.y, a.z);
+    }
+    f3 color = splat(0.0f);
+    uint32_t sIdx = 0, c = 0, done = 0;
+    uint32_t cur = 0, k = 0, base = 0, off = 0;
+    uint32_t cnt = P.ssgCount[(size_t)item0 * 64 + lane];
+    uint32_t h = 1;
+    uint32_t hStart = G > 1 ? ssg_start_word(P, item0 + 1, 0, lane) : 0xffffffffu;
+    while (done < total) {
+        while (h < G && off >= hStart + kWinPairs) {
+            ++h;
+            hStart = h < G ? ssg_start_word(P, item0 + h, 0, lane) : 0xffffffffu;
+        }
+        if (h < G && off >= hStart) {
+            const uint32_t w = off - hStart;
+            const unsigned long long* bits = P.ssgBits + (size_t)(item0 + h) * kWinWords * 64 + lane;
+            if ((bits[(w / 64) * 64] >> (w % 64)) & 1ull) {
+                uint32_t kh = __popcll(bits[(w / 64) * 64] & ((1ull << (w % 64)) - 1ull));
+                for (uint32_t j = 0; j < w / 64; ++j) kh += __popcll(bits[j * 64]);
+                const uint32_t ch = P.ssgCount[(size_t)(item0 + h) * 64 + lane];
+                if (kh < ch) {                                // continue in group h's log
+                    cur = h;
+                    k = kh;
+                    base = hStart;
+                    cnt = ch;
+                    ++h;
+                    hStart = h < G ? ssg_start_word(P, item0 + h, 0, lane) : 0xffffffffu;
+                    continue;
+                }
+            }
+        }
+        if (k >= cnt) break;
+        const size_t rec = (size_t)(item0 + cur) * P.ssgCap + k;
+        color = add(color, mk(P.ssgLog[(rec * 3 + 0) * 64 + lane], P.ssgLog[(rec * 3 + 1) * 64 + lane],
+                              P.ssgLog[(rec * 3 + 2) * 64 + lane]));
+        off = base + P.ssgEnd[rec * 64 + lane];
+        ++k;
+        ++done;
+        if (++sIdx == P.spp) {                                          // trace.cu:196
+            acc = (c == 0 && P.ignoreFirst) ? color : add(color, acc);
+            color = splat(0.0f);
+            sIdx = 0;
+            ++c;
+        }
+    }
+    Xorwow st;
+    if (cur == 0) {
+        st = {P.rng[li], P.rng[npix + li], P.rng[2 * npix + li], P.rng[3 * npix + li], P.rng[4 * npix + li],
+              P.rng[5 * npix + li]};
+    } else {
+        const uint32_t it = item0 + cur;
+        st = {ssg_start_word(P, it, 1, lane), ssg_start_word(P, it, 2, lane), ssg_start_word(P, it, 3, lane),
+              ssg_start_word(P, it, 4, lane), ssg_start_word(P, it, 5, lane), ssg_start_word(P, it, 6, lane)};
+    }
+    xorwow_skip(st, 2u * (off - base));
+    P.rng[li] = st.d;
+    P.rng[npix + li] = st.v0;
+    P.rng[2 * npix + li] = st.v1;
+    P.rng[3 * npix + li] = st.v2;
+    P.rng[4 * npix + li] = st.v3;
+    P.rng[5 * npix + li] = st.v4;
+    P.accum[li] = make_float4(acc.x, acc.y, acc.z, 1.0f);
+    if (done > 0) pairs[li] = (float)off / (float)done;
+    if (done < total) {
+        resume[li] = __float_as_uint(color.x);
+        resume[npix + li] = __float_as_uint(color.y);
+        resume[2 * npix + li] = __float_as_uint(color.z);
+        resume[3 * npix + li] = sIdx | (c << 16) | 0x80000000u;
+        atomicAdd(resumeCount, 1u);
+    } else {
+        resume[3 * npix + li] = 0u;
+    }
+}
+
 // Multi-device gather, second half: scatter one device's received rows (its bands, in local row
 // order) into the full image.  A band is band-rows consecutive image rows in both buffers, so every
 // lane copies one float4 of a coalesced row.
@@ -1263,6 +1557,19 @@ struct pt_context {
     bool orderValid = false;      // `order` holds a cost-sorted permutation
     bool orderStale = true;       // rebuild it after the next launch (scene, texture or camera changed)
     int schedule = 0;             // 0 = cost-sorted tiles (default), 1 = row-major
+    // speculative sample groups
+    int ssgMode = 0;              // 0 = automatic, 1 = off, G >= 2 = always G groups (tests)
+    float* pairs = nullptr;       // per-pixel draw pairs per sample (start-offset guesses)
+    bool pairsValid = false;
+    uint32_t* ssgStart = nullptr;
+    unsigned long long* ssgBits = nullptr;
+    uint32_t* ssgCount = nullptr;
+    float* ssgLog = nullptr;
+    uint16_t* ssgEnd = nullptr;
+    uint32_t* resume = nullptr;   // [4][pixels]
+    uint32_t* resumeCount = nullptr;
+    size_t ssgItems = 0, ssgSamples = 0;   // allocated: items, and item x capacity sample records
+    uint32_t lastGroups = 0;      // groups of the last launch (0 = plain launch)
     pt_camera lastCam = {};
     std::string err;
 };
@@ -1297,16 +1604,16 @@ static int fail(pt_context* ctx, int code, const char* msg)
 }
 
 // Kernel variants (workgroup size, scene staged in LDS or read through the caches).
-template <bool STATS, int SL, int WPB, int WW, int MINW, bool PERSIST = false>
+template <bool STATS, int SL, int WPB, int WW, int MINW, bool PERSIST = false, int MODE = 0>
 static hipError_t launch_one(const TraceParams& P, hipStream_t stream)
 {
     const size_t nodeF4 = WW >= 3 ? 4 * (size_t)P.cnodeCount : 2 * (size_t)P.nodeCount;
     const size_t sceneBytes = ((SL >= 1 ? nodeF4 : 0) + (SL >= 2 ? 4 * (size_t)P.primCount : 0)) * sizeof(float4);
     const size_t lds = sceneBytes + (size_t)WPB * P.stackDepth * 64 * (WW >= 3 ? 8 : 4) + (size_t)WPB * 64 * 12;
-    if (WW >= 3 && P.cnodes == nullptr) return launch_one<STATS, SL, WPB, 1, MINW, PERSIST>(P, stream);  // no child-box layout
+    if (WW >= 3 && P.cnodes == nullptr) return MODE == 1 ? hipErrorInvalidValue : launch_one<STATS, SL, WPB, 1, MINW, PERSIST, MODE>(P, stream);  // no child-box layout
     if (lds > 160 * 1024) {
         // scene too large to stage in LDS: the same variant reading the scene through the caches
-        if (SL > 0) return launch_one<STATS, 0, WPB, WW, MINW, PERSIST>(P, stream);
+        if (SL > 0) return launch_one<STATS, 0, WPB, WW, MINW, PERSIST, MODE>(P, stream);
         return hipErrorInvalidValue;                   // the stacks alone exceed the LDS
     }
     // the dynamic-LDS limit is raised once per device (contexts on several devices may run on
@@ -1316,13 +1623,12 @@ static hipError_t launch_one(const TraceParams& P, hipStream_t stream)
     (void)hipGetDevice(&dev);
     const uint64_t bit = 1ull << (dev & 63);
     if (!(attrSet.load() & bit)) {
-        hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(&trace_kernel<STATS, SL, WPB, WW, MINW, PERSIST>),
+        hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(&trace_kernel<STATS, SL, WPB, WW, MINW, PERSIST, MODE>),
                                            hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
         if (e != hipSuccess) return e;
         attrSet.fetch_or(bit);
     }
-    const uint32_t tiles = P.tilesX * P.tilesY;
-    unsigned blocks = (tiles + WPB - 1) / WPB;
+    unsigned blocks = (P.numSlots + WPB - 1) / WPB;    // numSlots = tiles, or tiles x groups (SSG)
     if (PERSIST) {
         // resident workgroups per device, cached per instantiation; a grid that fits in one
         // pass gains nothing from the cursor and runs the plain kernel
@@ -1333,15 +1639,15 @@ static hipError_t launch_one(const TraceParams& P, hipStream_t stream)
             hipError_t e = hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
             if (e == hipSuccess)
                 e = hipOccupancyMaxActiveBlocksPerMultiprocessor(
-                    &perCu, reinterpret_cast<const void*>(&trace_kernel<STATS, SL, WPB, WW, MINW, PERSIST>), WPB * 64, lds);
+                    &perCu, reinterpret_cast<const void*>(&trace_kernel<STATS, SL, WPB, WW, MINW, PERSIST, MODE>), WPB * 64, lds);
             if (e != hipSuccess) return e;
             cap = std::max(cus, 1) * std::max(perCu, 1);
             resident[dev & 63].store(cap);
         }
-        if (blocks <= (unsigned)cap) return launch_one<STATS, SL, WPB, WW, MINW, false>(P, stream);
+        if (blocks <= (unsigned)cap) return launch_one<STATS, SL, WPB, WW, MINW, false, MODE>(P, stream);
         blocks = (unsigned)cap;
     }
-    trace_kernel<STATS, SL, WPB, WW, MINW, PERSIST><<<blocks, WPB * 64, lds, stream>>>(P);
+    trace_kernel<STATS, SL, WPB, WW, MINW, PERSIST, MODE><<<blocks, WPB * 64, lds, stream>>>(P);
     return hipGetLastError();
 }
 
@@ -1356,17 +1662,30 @@ static hipError_t launch_one(const TraceParams& P, hipStream_t stream)
 //   40  default: resumable lean child-box walk, records in LDS, persistent waves, exit <= 24/64
 //   41  default for cache-read scenes: same, records through the caches, exit <= 12/64
 //   46  default for deep cache-read BVHs: variant 41 compiled for 4 waves/SIMD (128 VGPRs)
-template <bool STATS>
+template <bool STATS, int MODE = 0>
 static hipError_t launch_variant(int v, const TraceParams& P, hipStream_t stream)
 {
     switch (v) {
-    case 1: return launch_one<STATS, 0, 4, 0, 1>(P, stream);
-    case 4: return launch_one<STATS, 0, 4, 1, 5>(P, stream);
-    case 6: return launch_one<STATS, 1, 4, 1, 5>(P, stream);
-    case 20: return launch_one<STATS, 0, 4, 3, 5>(P, stream);
-    case 40: return launch_one<STATS, 1, 4, 224, 5, true>(P, stream);
-    case 41: return launch_one<STATS, 0, 4, 212, 5, true>(P, stream);
-    case 46: return launch_one<STATS, 0, 4, 212, 4, true>(P, stream);
+    case 1: return launch_one<STATS, 0, 4, 0, 1, false, MODE>(P, stream);
+    case 4: return launch_one<STATS, 0, 4, 1, 5, false, MODE>(P, stream);
+    case 6: return launch_one<STATS, 1, 4, 1, 5, false, MODE>(P, stream);
+    case 20: return launch_one<STATS, 0, 4, 3, 5, false, MODE>(P, stream);
+    case 40: return launch_one<STATS, 1, 4, 224, 5, true, MODE>(P, stream);
+    case 41: return launch_one<STATS, 0, 4, 212, 5, true, MODE>(P, stream);
+    case 46: return launch_one<STATS, 0, 4, 212, 4, true, MODE>(P, stream);
+    default: return hipErrorInvalidValue;
+    }
+}
+
+// Speculative-group launches (MODE 1) and their resume / pre-pass launches (MODE 2) exist for the
+// default variants only.
+template <int MODE>
+static hipError_t launch_grouped(int v, const TraceParams& P, hipStream_t stream)
+{
+    switch (v) {
+    case 40: return launch_one<false, 1, 4, 224, 5, true, MODE>(P, stream);
+    case 41: return launch_one<false, 0, 4, 212, 5, true, MODE>(P, stream);
+    case 46: return launch_one<false, 0, 4, 212, 4, true, MODE>(P, stream);
     default: return hipErrorInvalidValue;
     }
 }
@@ -1491,6 +1810,14 @@ PT_API void pt_destroy(pt_context* ctx)
     (void)hipFree(ctx->sortTemp);
     (void)hipFree(ctx->texTable);
     (void)hipFree(ctx->stats);
+    (void)hipFree(ctx->pairs);
+    (void)hipFree(ctx->ssgStart);
+    (void)hipFree(ctx->ssgBits);
+    (void)hipFree(ctx->ssgCount);
+    (void)hipFree(ctx->ssgLog);
+    (void)hipFree(ctx->ssgEnd);
+    (void)hipFree(ctx->resume);
+    (void)hipFree(ctx->resumeCount);
     for (auto& t : ctx->hostTex) (void)hipFree((void*)t.texels);
     if (ctx->ev0) (void)hipEventDestroy(ctx->ev0);
     if (ctx->ev1) (void)hipEventDestroy(ctx->ev1);
@@ -1650,6 +1977,65 @@ PT_API int pt_set_skybox(pt_context* ctx, uint32_t handle)
     return PT_OK;
 }
 
+// Speculative sample groups: how many groups a launch uses (0 = a plain launch).  A launch of
+// `tiles` 8x8 tiles on a chip with `resident` wave slots runs the plain kernel while it has at least
+// four tiles per slot (the cost-sorted list schedule then balances); with fewer, each pixel's chain is
+// cut into enough groups for about six work items per slot, each group at least 32 samples long.
+static uint32_t ssg_groups(const pt_context* ctx, int variant, uint32_t tiles, uint32_t total)
+{
+    if (ctx->ssgMode == 1 || (variant != 40 && variant != 41 && variant != 46)) return 0;
+    if (ctx->ssgMode >= 2) return std::min<uint32_t>((uint32_t)ctx->ssgMode, std::max(total, 1u));
+    int cus = 0;
+    if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, ctx->device) != hipSuccess) return 0;
+    const uint64_t resident = (uint64_t)cus * 4 * (variant == 46 ? 4 : 5);
+    if ((uint64_t)tiles >= 4 * resident) return 0;
+    uint64_t g = (6 * resident + tiles - 1) / tiles;
+    g = std::min<uint64_t>({g, 16, total / 32});
+    return g >= 2 ? (uint32_t)g : 0;
+}
+
+// Grow-only device buffers of the speculative groups; false if the device is out of memory (the
+// launch then runs plain).
+static bool ssg_reserve(pt_context* ctx, size_t items, size_t samples)
+{
+    const size_t npix = (size_t)ctx->rows * ctx->width;
+    if (!ctx->pairs) {
+        if (hipMalloc(&ctx->pairs, npix * sizeof(float)) != hipSuccess) return false;
+        if (hipMalloc(&ctx->resume, 4 * npix * sizeof(uint32_t)) != hipSuccess) return false;
+        if (hipMalloc(&ctx->resumeCount, sizeof(uint32_t)) != hipSuccess) return false;
+    }
+    if (items > ctx->ssgItems) {
+        (void)hipFree(ctx->ssgStart);
+        (void)hipFree(ctx->ssgBits);
+        (void)hipFree(ctx->ssgCount);
+        ctx->ssgStart = nullptr;
+        ctx->ssgBits = nullptr;
+        ctx->ssgCount = nullptr;
+        ctx->ssgItems = 0;
+        if (hipMalloc(&ctx->ssgStart, items * 7 * 64 * sizeof(uint32_t)) != hipSuccess ||
+            hipMalloc(&ctx->ssgBits, items * kWinWords * 64 * sizeof(unsigned long long)) != hipSuccess ||
+            hipMalloc(&ctx->ssgCount, items * 64 * sizeof(uint32_t)) != hipSuccess) {
+            (void)hipGetLastError();
+            return false;
+        }
+        ctx->ssgItems = items;
+    }
+    if (samples > ctx->ssgSamples) {
+        (void)hipFree(ctx->ssgLog);
+        (void)hipFree(ctx->ssgEnd);
+        ctx->ssgLog = nullptr;
+        ctx->ssgEnd = nullptr;
+        ctx->ssgSamples = 0;
+        if (hipMalloc(&ctx->ssgLog, samples * 64 * 3 * sizeof(float)) != hipSuccess ||
+            hipMalloc(&ctx->ssgEnd, samples * 64 * sizeof(uint16_t)) != hipSuccess) {
+            (void)hipGetLastError();
+            return false;
+        }
+        ctx->ssgSamples = samples;
+    }
+    return true;
+}
+
 static int render_impl(pt_context* ctx, const pt_camera* cam, uint32_t spp, uint32_t chunks, int ignore, float* gpu_ms,
                        pt_render_stats* stats)
 {
@@ -1748,20 +2134,34 @@ static int render_impl(pt_context* ctx, const pt_camera* cam, uint32_t spp, uint
     P.tileCursor = ctx->tileCursor;
     P.numSlots = tiles;
     if (stats) PT_HIP_CHECK(ctx, hipMemsetAsync(ctx->stats, 0, 16 * sizeof(unsigned long long), ctx->stream));
-    PT_HIP_CHECK(ctx, hipEventRecord(ctx->ev0, ctx->stream));
     const int variant = pick_variant(ctx);
+    // speculative sample groups
+    const uint32_t total = spp * chunks;
+    uint32_t G = (!stats && sorted && (uint64_t)spp * chunks < (1ull << 31)) ? ssg_groups(ctx, variant, tiles, total) : 0;
+    uint32_t ssgN = 0, ssgCap = 0;
+    if (G) {
+        ssgN = total / G;
+        ssgCap = std::min<uint32_t>(total, ssgN + std::max<uint32_t>(512u, ssgN / 4));
+        ssgCap = std::min<uint32_t>(ssgCap, 10000u);       // end offsets are 16-bit draw pairs (<= 6 per sample)
+        const uint32_t lastN = total - (G - 1) * ssgN;
+        if (lastN > ssgCap || !ssg_reserve(ctx, (size_t)tiles * G, (size_t)tiles * G * ssgCap)) G = 0;
+    }
+    ctx->lastGroups = G;
+    PT_HIP_CHECK(ctx, hipEventRecord(ctx->ev0, ctx->stream));
     if (sorted && (ctx->orderStale || !ctx->orderValid) && (uint64_t)spp * chunks >= kPrepassMinSpp && !stats) {
         // Cold start (first launch, or the scene, a texture or the camera changed): a short cost
         // pre-pass measures every tile -- kPrepassSpp samples per pixel from the pixels' current RNG
         // state, nothing written back (discard) -- and the launch below already runs in cost order.
         // Progressive 1-spp frames skip it and reuse the previous order for one launch instead.
         TraceParams Q = P;
-        Q.spp = kPrepassSpp;
+        Q.spp = G ? 8u : kPrepassSpp;              // speculative groups also take their offset guesses from it
         Q.chunks = 1;
         Q.ignoreFirst = 1;
         Q.discard = 1;
         Q.order = nullptr;
-        PT_HIP_CHECK(ctx, launch_variant<false>(variant, Q, ctx->stream));
+        Q.pairsOut = G ? ctx->pairs : nullptr;
+        if (G) ctx->pairsValid = true;
+        PT_HIP_CHECK(ctx, G ? launch_grouped<2>(variant, Q, ctx->stream) : launch_variant<false>(variant, Q, ctx->stream));
         size_t bytes = ctx->sortTempBytes;
         PT_HIP_CHECK(ctx, rocprim::radix_sort_pairs_desc(ctx->sortTemp, bytes, ctx->tileCost, ctx->sortKeys, ctx->tileIds,
                                                          ctx->order, tiles, 0, 32, ctx->stream));
@@ -1769,7 +2169,38 @@ static int render_impl(pt_context* ctx, const pt_camera* cam, uint32_t spp, uint
         ctx->orderStale = false;
         P.order = ctx->order;
     }
-    PT_HIP_CHECK(ctx, stats ? launch_variant<true>(variant, P, ctx->stream) : launch_variant<false>(variant, P, ctx->stream));
+    if (G) {
+        const size_t items = (size_t)tiles * G;
+        const unsigned pixBlocks = (unsigned)(((size_t)tiles * 64 + 255) / 256);
+        P.ssgG = G;
+        P.ssgCap = ssgCap;
+        P.ssgLastN = total - (G - 1) * ssgN;
+        P.ssgLog = ctx->ssgLog;
+        P.ssgEnd = ctx->ssgEnd;
+        P.ssgStart = ctx->ssgStart;
+        P.ssgBits = ctx->ssgBits;
+        P.ssgCount = ctx->ssgCount;
+        P.numSlots = (uint32_t)items;
+        PT_HIP_CHECK(ctx, hipMemsetAsync(ctx->ssgBits, 0, items * kWinWords * 64 * sizeof(unsigned long long), ctx->stream));
+        PT_HIP_CHECK(ctx, hipMemsetAsync(ctx->resumeCount, 0, sizeof(uint32_t), ctx->stream));
+        if (P.tileCost) PT_HIP_CHECK(ctx, hipMemsetAsync(P.tileCost, 0, (size_t)tiles * sizeof(uint32_t), ctx->stream));
+        ssg_guess_kernel<<<pixBlocks, 256, 0, ctx->stream>>>(P, ctx->pairsValid ? ctx->pairs : nullptr, ssgN, ctx->ssgStart);
+        PT_HIP_CHECK(ctx, hipGetLastError());
+        PT_HIP_CHECK(ctx, launch_grouped<1>(variant, P, ctx->stream));
+        ssg_fold_kernel<<<pixBlocks, 256, 0, ctx->stream>>>(P, ctx->resume, ctx->pairs, ctx->resumeCount);
+        PT_HIP_CHECK(ctx, hipGetLastError());
+        ctx->pairsValid = true;
+        // the samples the logs did not cover (if any): the plain kernel from the fold's state
+        TraceParams R = P;
+        R.ssgG = 0;
+        R.numSlots = tiles;
+        R.order = nullptr;
+        R.tileCost = nullptr;
+        R.resume = ctx->resume;
+        PT_HIP_CHECK(ctx, launch_grouped<2>(variant, R, ctx->stream));
+    } else {
+        PT_HIP_CHECK(ctx, stats ? launch_variant<true>(variant, P, ctx->stream) : launch_variant<false>(variant, P, ctx->stream));
+    }
     PT_HIP_CHECK(ctx, hipGetLastError());
     PT_HIP_CHECK(ctx, hipEventRecord(ctx->ev1, ctx->stream));
     PT_HIP_CHECK(ctx, hipEventSynchronize(ctx->ev1));
@@ -1805,6 +2236,28 @@ static int render_impl(pt_context* ctx, const pt_camera* cam, uint32_t spp, uint
         stats->cycles_total = h[14];
         stats->cycles_lane_idle = h[15];
     }
+    return PT_OK;
+}
+
+PT_API int pt_set_sample_groups(pt_context* ctx, int mode)
+{
+    if (!ctx || mode < 0 || mode > 4096) return PT_ERR_ARG;
+    ctx->ssgMode = mode;
+    return PT_OK;
+}
+
+PT_API int pt_last_sample_groups(const pt_context* ctx)
+{
+    return ctx ? (int)ctx->lastGroups : 0;
+}
+
+PT_API int pt_read_resume_count(pt_context* ctx, uint32_t* count)
+{
+    if (!ctx || !count) return PT_ERR_ARG;
+    *count = 0;
+    if (!ctx->resumeCount || ctx->lastGroups == 0) return PT_OK;
+    PT_HIP_CHECK(ctx, hipSetDevice(ctx->device));
+    PT_HIP_CHECK(ctx, hipMemcpy(count, ctx->resumeCount, sizeof(uint32_t), hipMemcpyDeviceToHost));
     return PT_OK;
 }
 

@@ -418,4 +418,22 @@ PT_DEV float uniform(Xorwow& s)   // curand_uniform: (0, 1]
     return (float)xorwow_next(s) * 2.3283064e-10f + (2.3283064e-10f / 2.0f);
 }
 
+// Advance by `draws` outputs (the values are not needed).  Used for the start states of speculative
+// sample groups; the draw count between two states of one stream is recovered from the Weyl word d,
+// which advances by 362437 per draw: draws = (d1 - d0) * kInvWeyl (mod 2^32).
+constexpr uint32_t kInvWeyl = 0x385e5f0du;     // 362437^-1 mod 2^32
+
+PT_DEV void xorwow_skip(Xorwow& s, uint32_t draws)
+{
+    for (uint32_t i = 0; i < draws; ++i) {
+        const uint32_t t = s.v0 ^ (s.v0 >> 2);
+        s.v0 = s.v1;
+        s.v1 = s.v2;
+        s.v2 = s.v3;
+        s.v3 = s.v4;
+        s.v4 = (s.v4 ^ (s.v4 << 4)) ^ (t ^ (t << 1));
+    }
+    s.d += 362437u * draws;
+}
+
 } // namespace pt

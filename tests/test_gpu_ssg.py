@@ -1,0 +1,74 @@
+"""Speculative sample groups: a pixel's sample chain cut into groups started at
+guessed draw offsets and stitched where the parses meet.  The bar is the same as for every other
+schedule: bit-identical accumulation sums and XORWOW states (trace.cu:183-198: one serial stream
+per pixel, the chunk fold color + accum)."""
+import numpy as np
+import pytest
+
+import pathtracercuda_amd as pa
+from oracle import pyoracle as po
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture(scope="module")
+def gpu_available():
+    if pa.device_count() < 1:
+        pytest.skip("no GPU")
+
+
+def bits(a):
+    return np.ascontiguousarray(a).view(np.uint32)
+
+
+def same(a, b, what):
+    if not np.array_equal(bits(a), bits(b)):
+        bad = np.argwhere(bits(a) != bits(b))
+        raise AssertionError(f"{what}: {len(bad)} words differ, first at {bad[0]}: {a[tuple(bad[0][:2])]} vs "
+                             f"{b[tuple(bad[0][:2])]}")
+
+
+@pytest.mark.parametrize("name,W,H,spp,chunks,groups", [
+    ("cornell_box", 64, 64, 8, 8, 2),
+    ("cornell_box", 37, 21, 3, 11, 5),        # ragged tiles, odd spp: the groups cut render() calls
+    ("generated_scene", 96, 54, 8, 16, 8),
+    ("test_shapes", 80, 50, 8, 8, 3),
+])
+def test_groups_bitexact_vs_oracle(gpu_available, scenes, name, W, H, spp, chunks, groups):
+    p = scenes / f"{name}.scene.json"
+    pt = pa.Pathtracer(W, H)
+    cam = pt.load_scene(str(p))
+    pt.set_sample_groups(groups)
+    pt.render(cam, spp, True, chunks=chunks)
+    assert pt.last_sample_groups == groups
+    osc = po.load_scene(p, W, H)
+    ref = po.OracleRenderer(osc, W, H)
+    ref.render(osc.camera, spp, True, chunks=chunks)
+    same(pt.accum(), ref.accum, f"{name} G={groups}")
+    assert np.array_equal(pt.rng_state(), ref.rng_array())
+    # a second launch continues the history (ignoreHistory = false) from the stitched state
+    pt.render(cam, spp, False, chunks=chunks)
+    ref.render(osc.camera, spp, False, chunks=chunks)
+    same(pt.accum(), ref.accum, f"{name} G={groups}, second launch")
+    assert np.array_equal(pt.rng_state(), ref.rng_array())
+
+
+def test_groups_equal_plain_launch_and_resume_path(gpu_available, scenes):
+    """One rank's share of the 1080p image at N = 8 (8-row bands): the automatic choice groups it; the
+    result equals the plain launch bit for bit.  Many groups over short chains force guesses that
+    miss, so the resume pass runs too."""
+    W, H = 1920, 1080
+    p = str(scenes / "generated_scene.scene.json")
+    out = {}
+    for mode in (1, 0, 16):
+        pt = pa.Pathtracer(W, H, row_offset=3, row_stride=8, band_rows=8)
+        cam = pt.load_scene(p)
+        pt.set_sample_groups(mode)
+        pt.render(cam, 8, True, chunks=32)
+        out[mode] = (pt.accum(), pt.rng_state(), pt.last_sample_groups, pt.resume_count())
+        pt.close()
+    assert out[1][2] == 0 and out[0][2] >= 2 and out[16][2] == 16
+    for mode in (0, 16):
+        same(out[mode][0], out[1][0], f"mode {mode}")
+        assert np.array_equal(out[mode][1], out[1][1])
+    assert out[16][3] > 0, "the resume pass was not exercised"
