@@ -194,10 +194,20 @@ PT_API int pt_set_schedule(pt_context *ctx, int mode);
  * groups, each pixel's chain is cut into G pieces started at guessed draw offsets and stitched where
  * the guessed parse meets the true one; results stay bit-identical.  mode: 0 = automatic (default),
  * 1 = never, G >= 2 = always G groups (tests).  pt_last_sample_groups: groups of the last launch
- * (0 = plain); pt_read_resume_count: pixels the last grouped launch finished in its resume pass. */
+ * (0 = plain).  pt_read_group_stats fills 10 words: G, patch rounds run, and the pixels at a dead end
+ * after fold rounds 0..7.  pt_read_group_log_counts: samples each (tile, item) logged per lane
+ * ([tile][2G - 1][64], tiles row-major over the context; item 0 = group 0, items 2g - 1 and 2g =
+ * group g at its guessed offset and one draw pair later).  pt_set_patch_rounds: patch rounds before
+ * the remaining dead ends run as a plain resume launch (default 6; 0 exercises the resume path). */
 PT_API int pt_set_sample_groups(pt_context *ctx, int mode);
+PT_API int pt_set_patch_rounds(pt_context *ctx, uint32_t rounds);
 PT_API int pt_last_sample_groups(const pt_context *ctx);
-PT_API int pt_read_resume_count(pt_context *ctx, uint32_t *count);
+PT_API int pt_read_group_stats(const pt_context *ctx, uint32_t *dst);
+PT_API int pt_read_group_log_counts(pt_context *ctx, uint32_t *dst, size_t count);
+/* Diagnostics: one word plane of the per-pixel fold state (rows x width; word 16 = dead-end flag,
+ * 7 = samples done, 8 = draw-pair offset), or with word 19 the draw pairs per sample (float) that
+ * the next launch's guesses use. */
+PT_API int pt_read_group_fold(pt_context *ctx, uint32_t word, uint32_t *dst);
 PT_API const char *pt_last_error(const pt_context *ctx);
 
 /* ---- Multi-device group (one process, one context per GPU, RCCL over xGMI) -------------------

@@ -264,11 +264,32 @@ class Pathtracer:
     def last_sample_groups(self) -> int:
         return int(N.hip().pt_last_sample_groups(self._ctx))
 
-    def resume_count(self) -> int:
-        """Pixels the last grouped launch finished in its resume pass."""
-        n = C.c_uint32(0)
-        N.check_ctx(N.hip().pt_read_resume_count(self._ctx, C.byref(n)), self._ctx)
-        return int(n.value)
+    def set_patch_rounds(self, rounds: int) -> None:
+        N.check_ctx(N.hip().pt_set_patch_rounds(self._ctx, int(rounds)), self._ctx)
+
+    def group_fold_word(self, word: int) -> np.ndarray:
+        """Diagnostics: a plane of the grouped launch's fold state (pt_read_group_fold); word 19 =
+        draw pairs per sample (float32)."""
+        out = np.zeros((self.rows, self.width), dtype=np.uint32)
+        N.check_ctx(N.hip().pt_read_group_fold(self._ctx, int(word), out.ctypes.data_as(C.POINTER(C.c_uint32))), self._ctx)
+        return out.view(np.float32) if word == 19 else out
+
+    def group_stats(self) -> Dict[str, object]:
+        """How the last grouped launch went: groups, patch rounds, dead-end pixels after each fold."""
+        out = (C.c_uint32 * 10)()
+        N.check_ctx(N.hip().pt_read_group_stats(self._ctx, out), self._ctx)
+        v = list(out)
+        return {"groups": v[0], "patch_rounds": v[1], "dead_ends": v[2:2 + v[1] + 1] if v[0] else []}
+
+    def group_log_counts(self) -> np.ndarray:
+        """Samples each (tile, item) of the last grouped launch logged: (tiles, 2 * groups - 1, 64);
+        item 0 = group 0, items 2g - 1 and 2g = group g at its guess and one draw pair later."""
+        g = 2 * self.last_sample_groups - 1
+        tiles = ((self.width + 7) // 8) * ((self.rows + 7) // 8)
+        out = np.zeros((tiles, g, 64), dtype=np.uint32)
+        N.check_ctx(N.hip().pt_read_group_log_counts(self._ctx, out.ctypes.data_as(C.POINTER(C.c_uint32)), out.size),
+                    self._ctx)
+        return out
 
     def tile_costs(self) -> np.ndarray:
         """Shader-clock cycles of each 8x8 tile in the last launch (tiles_y x tiles_x)."""

@@ -73,7 +73,10 @@ _HIP_SYMBOLS = {
     "pt_set_schedule": (C.c_int, [C.c_void_p, C.c_int]),
     "pt_set_sample_groups": (C.c_int, [C.c_void_p, C.c_int]),
     "pt_last_sample_groups": (C.c_int, [C.c_void_p]),
-    "pt_read_resume_count": (C.c_int, [C.c_void_p, P(C.c_uint32)]),
+    "pt_read_group_stats": (C.c_int, [C.c_void_p, P(C.c_uint32)]),
+    "pt_set_patch_rounds": (C.c_int, [C.c_void_p, C.c_uint32]),
+    "pt_read_group_fold": (C.c_int, [C.c_void_p, C.c_uint32, P(C.c_uint32)]),
+    "pt_read_group_log_counts": (C.c_int, [C.c_void_p, P(C.c_uint32), C.c_size_t]),
     "pt_last_error": (C.c_char_p, [C.c_void_p]),
     "pt_group_create": (C.c_int, [C.c_int, P(C.c_int), C.c_uint32, C.c_uint32, C.c_uint32, P(C.c_void_p)]),
     "pt_group_destroy": (None, [C.c_void_p]),

@@ -81,24 +81,31 @@ struct TraceParams {
     uint32_t* tileCost;         // per-tile shader-clock cycles of this launch (null: not recorded)
     uint32_t discard;           // != 0: cost pre-pass -- pixel state (RNG, accum) is read, never written
     float* pairsOut;            // cost pre-pass: per-pixel draw pairs per sample (speculative groups' guess)
-    // Speculative sample groups (0 = off).  Work item = (tile, group g): slot s runs
-    // tile order[s / ssgG], group s % ssgG; item index = tile * ssgG + g.
+    // Speculative sample groups (0 = off).  A tile has J = 2G - 1 work items: item 0 =
+    // group 0; items 2g - 1 and 2g = group g >= 1 started at its guessed draw offset and, for pixels
+    // whose sample starts sit on the even lattice with rare odd shifts, one pair later (else that
+    // lane is idle).  Slot s runs tile order[s / J], item s % J; item index = tile * J + j.  Patch
+    // rounds (ssgPatch): one carrier per tile, lanes = the pixels the fold left at a dead end.
     uint32_t ssgG;              // groups per pixel
     uint32_t ssgCap;            // sample-log capacity per item
-    uint32_t ssgLastN;          // the last group stops after this many samples
+    uint32_t ssgPatch;          // != 0: patch round
     float* ssgLog;              // [item][cap][3][64] path colours
     uint16_t* ssgEnd;           // [item][cap][64] end of each sample, in draw pairs from the item's start
-    const uint32_t* ssgStart;   // [item][7][64] start offset (draw pairs), then the state d, v0..v4
-    unsigned long long* ssgBits;// [item][kWinWords][64] the item's sample starts in its first kWinPairs pairs
+    const uint32_t* ssgStart;   // [item][8][64] start offset (draw pairs; ~0 = idle lane), d, v0..v4, stop offset
+    unsigned long long* ssgBits;// [item][kWinWords][64] the item's sample starts in its window
     uint32_t* ssgCount;         // [item][64] samples logged
-    const uint32_t* resume;     // resume launch: [4][rows*width] colour x/y/z bits, s | c << 16 | valid << 31
+    uint32_t* fold;             // [kFoldWords][rows*width] fold state (ssg_fold_kernel); AUX resume input
     DevCamera cam;
 };
 
 // Speculative sample groups: window of a group's start offset in which an earlier group's parse can
-// join it (draw pairs; 8 x 64-bit words per lane).
-constexpr uint32_t kWinWords = 8;
+// join it (draw pairs; 16 x 64-bit words per lane), and the fold state kept per pixel between rounds.
+constexpr uint32_t kWinWords = 16;
 constexpr uint32_t kWinPairs = 64 * kWinWords;
+constexpr uint32_t kFoldBatch = 16;       // samples the fold loads at once
+constexpr uint32_t kStartWords = 8;       // start record: offset, d, v0..v4, stop offset (last group)
+enum : uint32_t { F_ACC = 0, F_COL = 3, F_SC = 6, F_DONE = 7, F_OFF = 8, F_H = 9, F_ST = 10, F_FLAG = 16, F_ODD = 17,
+                  F_SQ = 18, kFoldWords = 19 };
 
 // Row tiling of an image across contexts (multi-GPU): the image is cut into bands of
 // B = 1 << shift rows, and a context owns bands b = offset + k * stride.  Local row ly lies in the
@@ -1047,65 +1054,106 @@ PT_DEV uint32_t wave_fetch(uint32_t* cursor, uint32_t n)
 // final state; whatever the logs do not cover runs in a resume launch.  Results are bit-identical.
 // ---------------------------------------------------------------------------------------------
 struct SsgLane {
-    uint32_t item;      // tile * G + g
-    uint32_t g;
+    uint32_t logItem;   // index into the log arrays: tile * J + j, or the tile in a patch round
+    uint32_t grp0;      // tile * J: the items of this tile
+    uint32_t g;         // group index; G in a patch round (no window of its own)
     uint32_t k;         // samples logged
     uint32_t d0;        // Weyl word at the item's start
     uint32_t base;      // start offset of the item (draw pairs)
     uint32_t h;         // next group whose window this parse may reach (G: none)
     uint32_t hStart;    // its start offset
     uint32_t limit;     // samples before the item stops regardless
+    uint32_t stopOff;   // the last group stops at this draw-pair offset (~0: none)
 };
 
 PT_DEV uint32_t ssg_start_word(const TraceParams& P, uint32_t item, uint32_t w, uint32_t lane)
 {
-    return P.ssgStart[((size_t)item * 7 + w) * 64 + lane];
+    return P.ssgStart[((size_t)item * kStartWords + w) * 64 + lane];
 }
 
 PT_DEV void ssg_load(const TraceParams& P, uint32_t tile, uint32_t g, uint32_t lane, size_t li, size_t npix,
                      Xorwow& rng, PathState& ps, SsgLane& sl)
 {
-    sl.item = tile * P.ssgG + g;
-    sl.g = g;
+    const uint32_t G = P.ssgG;
+    sl.grp0 = tile * (2 * G - 1);
     sl.k = 0;
-    if (g == 0) {
-        rng.d = P.rng[li];
-        rng.v0 = P.rng[npix + li];
-        rng.v1 = P.rng[2 * npix + li];
-        rng.v2 = P.rng[3 * npix + li];
-        rng.v3 = P.rng[4 * npix + li];
-        rng.v4 = P.rng[5 * npix + li];
-        sl.base = 0;
-    } else {
-        sl.base = ssg_start_word(P, sl.item, 0, lane);
-        rng.d = ssg_start_word(P, sl.item, 1, lane);
-        rng.v0 = ssg_start_word(P, sl.item, 2, lane);
-        rng.v1 = ssg_start_word(P, sl.item, 3, lane);
-        rng.v2 = ssg_start_word(P, sl.item, 4, lane);
-        rng.v3 = ssg_start_word(P, sl.item, 5, lane);
-        rng.v4 = ssg_start_word(P, sl.item, 6, lane);
-        // the item's own start is its first sample start
-        __hip_atomic_fetch_or(&P.ssgBits[(size_t)sl.item * kWinWords * 64 + lane], 1ull, __ATOMIC_RELAXED,
-                              __HIP_MEMORY_SCOPE_AGENT);
-    }
-    sl.d0 = rng.d;
-    sl.h = g + 1;
-    sl.hStart = sl.h < P.ssgG ? ssg_start_word(P, sl.item + 1, 0, lane) : 0xffffffffu;
-    sl.limit = g + 1 == P.ssgG ? P.ssgLastN : P.ssgCap;
     ps.L = splat(0.0f);
     ps.T = splat(1.0f);
     ps.bounce = 0;
+    if (P.ssgPatch) {
+        // a carrier from the fold's dead end: the true state there, the fold's next candidate group
+        const uint32_t* F = P.fold;
+        sl.logItem = tile;
+        sl.g = G;
+        if (!(F[F_FLAG * npix + li] & 1u)) {       // finished pixel: its other fold words are stale
+            sl.limit = 0;
+            ps.alive = false;
+            sl.d0 = 0;
+            sl.base = 0;
+            sl.h = G;
+            sl.hStart = 0xffffffffu;
+            return;
+        }
+        sl.base = F[F_OFF * npix + li];
+        rng.d = F[(F_ST + 0) * npix + li];
+        rng.v0 = F[(F_ST + 1) * npix + li];
+        rng.v1 = F[(F_ST + 2) * npix + li];
+        rng.v2 = F[(F_ST + 3) * npix + li];
+        rng.v3 = F[(F_ST + 4) * npix + li];
+        rng.v4 = F[(F_ST + 5) * npix + li];
+        sl.h = min(F[F_H * npix + li], G);
+        sl.limit = min(P.ssgCap, P.spp * P.chunks - F[F_DONE * npix + li]);
+    } else {
+        const uint32_t j = g;                      // item index within the tile
+        g = (j + 1) >> 1;
+        sl.logItem = sl.grp0 + j;
+        sl.g = g;
+        if (g == 0) {
+            rng.d = P.rng[li];
+            rng.v0 = P.rng[npix + li];
+            rng.v1 = P.rng[2 * npix + li];
+            rng.v2 = P.rng[3 * npix + li];
+            rng.v3 = P.rng[4 * npix + li];
+            rng.v4 = P.rng[5 * npix + li];
+            sl.base = 0;
+        } else {
+            sl.base = ssg_start_word(P, sl.logItem, 0, lane);
+            if (sl.base == 0xffffffffu) {          // the second phase of a pixel that has none
+                sl.limit = 0;
+                ps.alive = false;
+                sl.d0 = 0;
+                sl.h = G;
+                sl.hStart = 0xffffffffu;
+                return;
+            }
+            rng.d = ssg_start_word(P, sl.logItem, 1, lane);
+            rng.v0 = ssg_start_word(P, sl.logItem, 2, lane);
+            rng.v1 = ssg_start_word(P, sl.logItem, 3, lane);
+            rng.v2 = ssg_start_word(P, sl.logItem, 4, lane);
+            rng.v3 = ssg_start_word(P, sl.logItem, 5, lane);
+            rng.v4 = ssg_start_word(P, sl.logItem, 6, lane);
+            // the group's own start is its first sample start
+            __hip_atomic_fetch_or(&P.ssgBits[(size_t)sl.logItem * kWinWords * 64 + lane], 1ull, __ATOMIC_RELAXED,
+                                  __HIP_MEMORY_SCOPE_AGENT);
+        }
+        sl.h = g + 1;
+        sl.limit = P.ssgCap;
+    }
+    sl.d0 = rng.d;
+    sl.hStart = sl.h < G ? ssg_start_word(P, sl.grp0 + 2 * sl.h - 1, 0, lane) : 0xffffffffu;
+    sl.stopOff = (!P.ssgPatch && sl.g + 1 == G) ? ssg_start_word(P, sl.logItem, 7, lane) : 0xffffffffu;
     ps.alive = sl.limit > 0;
 }
 
-// End of a path in a speculative group: log it, record the sample start that follows, stop at a
-// junction with a later group (or at the item's limit), else start the next sample.
+// End of a path in a speculative item: log it, record the sample start that follows (in the group's
+// own window), stop at a junction with a later group or at the item's limit, else start the next
+// sample.
 template <bool STATS>
 PT_DEV void ssg_finish(const TraceParams& P, PathState& ps, Xorwow& rng, float fx, float fy, SsgLane& sl,
                        uint32_t lane, Counters& cnt)
 {
     if (STATS) cnt.samples++;
-    const size_t rec = (size_t)sl.item * P.ssgCap + sl.k;
+    const size_t rec = (size_t)sl.logItem * P.ssgCap + sl.k;
     P.ssgLog[(rec * 3 + 0) * 64 + lane] = ps.L.x;
     P.ssgLog[(rec * 3 + 1) * 64 + lane] = ps.L.y;
     P.ssgLog[(rec * 3 + 2) * 64 + lane] = ps.L.z;
@@ -1113,20 +1161,33 @@ PT_DEV void ssg_finish(const TraceParams& P, PathState& ps, Xorwow& rng, float f
     P.ssgEnd[rec * 64 + lane] = (uint16_t)rel;
     ++sl.k;
     bool stop = sl.k >= sl.limit;
-    if (sl.g > 0 && rel < kWinPairs)
-        __hip_atomic_fetch_or(&P.ssgBits[((size_t)sl.item * kWinWords + rel / 64) * 64 + lane], 1ull << (rel % 64),
+    if (sl.g - 1u < P.ssgG - 1u && rel < kWinPairs)                    // groups 1 .. G-1
+        __hip_atomic_fetch_or(&P.ssgBits[((size_t)sl.logItem * kWinWords + rel / 64) * 64 + lane], 1ull << (rel % 64),
                               __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     const uint32_t off = sl.base + rel;
-    while (sl.h < P.ssgG && off >= sl.hStart + kWinPairs) {          // passed that group's window
+    stop = stop || off >= sl.stopOff;                                  // the last group: past the expected end
+    const uint32_t j = sl.logItem - sl.grp0;
+    if (!stop && j >= 2 && !(j & 1u) && !P.ssgPatch && rel + 1 < kWinPairs) {
+        // the second phase has joined the first one's parse (a sample start of item j - 1): from here
+        // the two are the same parse, the first carries on
+        const uint32_t wa = rel + 1;
+        stop = (__hip_atomic_load(&P.ssgBits[((size_t)(sl.logItem - 1) * kWinWords + wa / 64) * 64 + lane], __ATOMIC_RELAXED,
+                                  __HIP_MEMORY_SCOPE_AGENT) >> (wa % 64)) & 1ull;
+    }
+    while (sl.h < P.ssgG && off > sl.hStart + kWinPairs) {           // passed that group's windows
         ++sl.h;
-        sl.hStart = sl.h < P.ssgG ? ssg_start_word(P, sl.item - sl.g + sl.h, 0, lane) : 0xffffffffu;
+        sl.hStart = sl.h < P.ssgG ? ssg_start_word(P, sl.grp0 + 2 * sl.h - 1, 0, lane) : 0xffffffffu;
     }
     if (!stop && sl.h < P.ssgG && off >= sl.hStart) {
+        // junction: a sample start of group h's parse (either phase; an idle phase has no bits)
         const uint32_t w = off - sl.hStart;
-        const unsigned long long bits = __hip_atomic_load(
-            &P.ssgBits[((size_t)(sl.item - sl.g + sl.h) * kWinWords + w / 64) * 64 + lane], __ATOMIC_RELAXED,
-            __HIP_MEMORY_SCOPE_AGENT);
-        stop = (bits >> (w % 64)) & 1ull;                              // junction: group h carries on
+        const size_t itA = sl.grp0 + 2 * sl.h - 1;
+        if (w < kWinPairs)
+            stop = (__hip_atomic_load(&P.ssgBits[(itA * kWinWords + w / 64) * 64 + lane], __ATOMIC_RELAXED,
+                                      __HIP_MEMORY_SCOPE_AGENT) >> (w % 64)) & 1ull;
+        if (!stop && w >= 1)
+            stop = (__hip_atomic_load(&P.ssgBits[((itA + 1) * kWinWords + (w - 1) / 64) * 64 + lane], __ATOMIC_RELAXED,
+                                      __HIP_MEMORY_SCOPE_AGENT) >> ((w - 1) % 64)) & 1ull;
     }
     if (stop) {
         ps.alive = false;
@@ -1179,7 +1240,7 @@ PT_DEV void load_pixel(const TraceParams& P, const PixelCtx& pc, Xorwow& rng, Pa
     rng.v3 = P.rng[4 * pc.npix + pc.li];
     rng.v4 = P.rng[5 * pc.npix + pc.li];
     ps.acc = accL;
-    if (!P.ignoreFirst || (AUX && P.resume)) {   // the first call of an ignoreHistory launch overwrites it
+    if (!P.ignoreFirst || (AUX && P.fold)) {     // the first call of an ignoreHistory launch overwrites it
         const float4 a = P.accum[pc.li];
         float* l = lds_f() + accL;
         l[0] = a.x;
@@ -1191,12 +1252,13 @@ PT_DEV void load_pixel(const TraceParams& P, const PixelCtx& pc, Xorwow& rng, Pa
     ps.T = splat(1.0f);
     ps.s = ps.c = ps.bounce = 0;
     ps.alive = P.chunks > 0 && P.spp > 0;
-    if (AUX && P.resume) {                       // mid-launch state left by ssg_fold_kernel
-        ps.color = mk(__uint_as_float(P.resume[pc.li]), __uint_as_float(P.resume[pc.npix + pc.li]),
-                      __uint_as_float(P.resume[2 * pc.npix + pc.li]));
-        const uint32_t sc = P.resume[3 * pc.npix + pc.li];
+    if (AUX && P.fold) {                         // mid-launch state left by ssg_fold_kernel
+        const uint32_t* F = P.fold;
+        ps.color = mk(__uint_as_float(F[(F_COL + 0) * pc.npix + pc.li]), __uint_as_float(F[(F_COL + 1) * pc.npix + pc.li]),
+                      __uint_as_float(F[(F_COL + 2) * pc.npix + pc.li]));
+        const uint32_t sc = F[F_SC * pc.npix + pc.li];
         ps.s = sc & 0xffffu;
-        ps.c = (sc >> 16) & 0x7fffu;
+        ps.c = sc >> 16;
         ps.alive = ps.c < P.chunks;
     }
 }
@@ -1254,16 +1316,17 @@ __global__ void __launch_bounds__(WPB * 64, MINW) trace_kernel(TraceParams P)
     for (;;) {
     if (PERSIST && slot >= P.numSlots) break;
     uint32_t tile, grp = 0;
-    if (SSG) {
-        const uint32_t ts = slot / P.ssgG;
-        grp = slot - ts * P.ssgG;
+    if (SSG && !P.ssgPatch) {
+        const uint32_t J = 2 * P.ssgG - 1;
+        const uint32_t ts = slot / J;
+        grp = slot - ts * J;                         // item within the tile (ssg_load)
         tile = P.order ? P.order[ts] : ts;
     } else {
         tile = P.order ? P.order[slot] : slot;
     }
     const PixelCtx pc = pixel_of(P, tile, lane);
     const uint64_t tWave = __builtin_amdgcn_s_memtime();
-    const bool run = pc.valid && (!AUX || !P.resume || (P.resume[3 * pc.npix + pc.li] >> 31));
+    const bool run = pc.valid && (!AUX || !P.fold || (P.fold[F_FLAG * pc.npix + pc.li] & 1u));
     if (run) {
         Xorwow rng;
         PathState ps;
@@ -1306,14 +1369,17 @@ __global__ void __launch_bounds__(WPB * 64, MINW) trace_kernel(TraceParams P)
         }
         if (STATS && WW >= 100 && tDone) cnt.cyc_lane_idle += __builtin_amdgcn_s_memtime() - tDone;
         if (STATS) wave_time(cnt.cyc_total, tAll);
-        if (SSG) P.ssgCount[(size_t)sl.item * 64 + lane] = sl.k;
+        if (SSG) P.ssgCount[(size_t)sl.logItem * 64 + lane] = sl.k;
         else if (!P.discard) store_pixel(P, pc, rng, ps);
         else if (AUX && P.pairsOut)           // cost pre-pass: draw pairs per sample of this pixel
+        {
             P.pairsOut[pc.li] = (float)(((rng.d - P.rng[pc.li]) * kInvWeyl) >> 1) / (float)(P.spp * P.chunks);
+            P.pairsOut[pc.npix + pc.li] = -1.0f;      // odd-length fraction unknown
+        }
     }
     if (P.tileCost && lane == 0 && tile < P.tilesX * P.tilesY) {
         const uint32_t cyc = (uint32_t)min(__builtin_amdgcn_s_memtime() - tWave, (uint64_t)0xffffffffu);
-        if (SSG) atomicAdd(&P.tileCost[tile], cyc / P.ssgG);   // zeroed before the launch
+        if (SSG) atomicAdd(&P.tileCost[tile], cyc / P.ssgG);   // zeroed before the launch (idle items add ~0)
         else P.tileCost[tile] = cyc;
     }
     if (!PERSIST) break;
@@ -1395,15 +1461,33 @@ __global__ void __launch_bounds__(256) ssg_guess_kernel(TraceParams P, const flo
     const size_t npix = (size_t)P.rows * P.width;
     Xorwow st = {P.rng[li], P.rng[npix + li], P.rng[2 * npix + li], P.rng[3 * npix + li], P.rng[4 * npix + li],
                  P.rng[5 * npix + li]};
+    const size_t npixAll = (size_t)P.rows * P.width;
     float m = pairs ? pairs[li] : 2.0f;
     m = (m >= 1.0f) ? fminf(m, 6.0f) : 1.0f;       // 1..6 pairs per sample (jitter + up to 5 hits)
+    const float podd = pairs ? pairs[npixAll + li] : -1.0f;   // fraction of odd-length samples (< 0: unknown)
+    const float var = (pairs && podd >= 0.0f) ? pairs[2 * npixAll + li] : 1.0f;   // variance of pairs per sample
+    // the last group stops once its parse passes the expected end of the pixel's chain plus three
+    // standard deviations (a short tail is finished by a patch round)
+    const float total = (float)(P.spp * P.chunks);
+    const uint32_t stopOff = (uint32_t)(total * m + 3.0f * sqrtf(total * fmaxf(var, 0.05f)) + 2.0f);
+    // A pixel whose samples rarely take an odd number of pairs (< 6 %; ground under open sky: 2, or
+    // 2 and 4) keeps its true sample starts on one parity for long stretches; a rare odd sample
+    // flips it.  Its guesses sit on even offsets, and a second item starts one pair later, so the
+    // parse that joins exists whatever the parity of the true one.  Other near-integer means q >= 3
+    // use their own lattice (single item).
+    const bool parityStable = podd >= 0.0f ? podd < 0.06f : fabsf(m - 2.0f) < 0.25f;
+    const float q = parityStable ? 2.0f : rintf(m);
+    const bool lattice = parityStable || (q >= 3.0f && fabsf(m - q) < 0.02f);
+    const bool dual = parityStable && m > 1.5f;
+    const uint32_t J = 2 * P.ssgG - 1;
     uint32_t off = 0;
     for (uint32_t g = 1; g < P.ssgG; ++g) {
-        uint32_t o = (uint32_t)((float)(g * n) * m + 0.5f);
+        uint32_t o = lattice ? (uint32_t)q * (uint32_t)((float)(g * n) * (m / q) + 0.5f)
+                             : (uint32_t)((float)(g * n) * m + 0.5f);
         if (o <= off) o = off + 1;
         xorwow_skip(st, 2u * (o - off));
         off = o;
-        uint32_t* w = start + (size_t)(tile * P.ssgG + g) * 7 * 64 + lane;
+        uint32_t* w = start + ((size_t)tile * J + 2 * g - 1) * kStartWords * 64 + lane;
         w[0] = o;
         w[64] = st.d;
         w[128] = st.v0;
@@ -1411,73 +1495,210 @@ __global__ void __launch_bounds__(256) ssg_guess_kernel(TraceParams P, const flo
         w[256] = st.v2;
         w[320] = st.v3;
         w[384] = st.v4;
+        w[448] = g + 1 == P.ssgG ? stopOff : 0xffffffffu;
+        uint32_t* w2 = w + kStartWords * 64;       // the item one pair later
+        if (dual) {
+            Xorwow s2 = st;
+            xorwow_skip(s2, 2u);
+            w2[0] = o + 1;
+            w2[64] = s2.d;
+            w2[128] = s2.v0;
+            w2[192] = s2.v1;
+            w2[256] = s2.v2;
+            w2[320] = s2.v3;
+            w2[384] = s2.v4;
+            w2[448] = g + 1 == P.ssgG ? stopOff : 0xffffffffu;
+        } else {
+            w2[0] = 0xffffffffu;
+        }
     }
 }
 
-// Walk each pixel's true parse through the logs: from group 0, at every sample start check whether a
-// later group's parse has a sample start there (its window bits) and, if that group logged samples
-// from there, continue in its log.  Colours are summed per render() call and folded into the
-// accumulation value exactly as trace.cu:186-198 does; the final XORWOW state is the state at the
-// last consumed sample's end (the item's start state advanced by the draws since).  Pixels whose logs
-// end before spp x chunks samples get a resume record (and a resume launch runs the rest).
-__global__ void __launch_bounds__(256) ssg_fold_kernel(TraceParams P, uint32_t* __restrict__ resume,
-                                                       float* __restrict__ pairs, uint32_t* __restrict__ resumeCount)
+// Walk each pixel's true parse through the logs.  Round 0 starts at group 0 (the pixel's own state);
+// a later round starts in the patch log of the carrier that ran from the previous round's dead end.
+// At every sample start the walk checks whether a later group's parse has a sample start there (its
+// window bits) and, if that group logged samples from there, continues in its log.  Colours are summed
+// per render() call and folded into the accumulation value exactly as trace.cu:186-198 does.  Where
+// the logs end first (a dead end), the state is kept for the next round: the exact XORWOW state there
+// (the item's start state advanced by the draws since), the partial sums, the next candidate group.
+__global__ void __launch_bounds__(256) ssg_fold_kernel(TraceParams P, uint32_t round, const float* __restrict__ patchLog,
+                                                       const uint16_t* __restrict__ patchEnd,
+                                                       const uint32_t* __restrict__ patchCount, uint32_t patchCap,
+                                                       float* __restrict__ pairs, uint32_t* __restrict__ deadCount)
 {
     uint32_t tile, lane;
     size_t li;
     if (!ssg_pixel(P, (size_t)blockIdx.x * 256 + threadIdx.x, tile, lane, li)) return;
     const size_t npix = (size_t)P.rows * P.width;
-    const uint32_t G = P.ssgG, item0 = tile * G, total = P.spp * P.chunks;
-    f3 acc = splat(0.0f);
-    if (!P.ignoreFirst) {
-        const float4 a = P.accum[li];
-        acc = mk(a.x, a.y, a.z);
+    uint32_t* F = P.fold;
+    const uint32_t G = P.ssgG, item0 = tile * (2 * G - 1), total = P.spp * P.chunks;
+    f3 acc, color;
+    uint32_t sIdx, c, done, off, h, odd = 0, prevRel = 0, sq = 0;
+    bool inPatch;
+    uint32_t cur, k, base, cnt;
+    if (round == 0) {
+        acc = splat(0.0f);
+        if (!P.ignoreFirst) {
+            const float4 a = P.accum[li];
+            acc = mk(a.x, a.y, a.z);
+        }
+        color = splat(0.0f);
+        sIdx = c = done = off = 0;
+        h = 1;
+        inPatch = false;
+        cur = 0;
+        k = 0;
+        base = 0;
+        cnt = P.ssgCount[(size_t)item0 * 64 + lane];
+    } else {
+        if (!(F[F_FLAG * npix + li] & 1u)) return;
+        acc = mk(__uint_as_float(F[(F_ACC + 0) * npix + li]), __uint_as_float(F[(F_ACC + 1) * npix + li]),
+                 __uint_as_float(F[(F_ACC + 2) * npix + li]));
+        color = mk(__uint_as_float(F[(F_COL + 0) * npix + li]), __uint_as_float(F[(F_COL + 1) * npix + li]),
+                   __uint_as_float(F[(F_COL + 2) * npix + li]));
+        const uint32_t sc = F[F_SC * npix + li];
+        sIdx = sc & 0xffffu;
+        c = sc >> 16;
+        done = F[F_DONE * npix + li];
+        off = F[F_OFF * npix + li];
+        h = min(F[F_H * npix + li], G);
+        odd = F[F_ODD * npix + li];
+        sq = F[F_SQ * npix + li];
+        inPatch = true;
+        cur = G;
+        k = 0;
+        base = off;
+        cnt = patchCount[(size_t)tile * 64 + lane];
     }
-    f3 color = splat(0.0f);
-    uint32_t sIdx = 0, c = 0, done = 0;
-    uint32_t cur = 0, k = 0, base = 0, off = 0;
-    uint32_t cnt = P.ssgCount[(size_t)item0 * 64 + lane];
-    uint32_t h = 1;
-    uint32_t hStart = G > 1 ? ssg_start_word(P, item0 + 1, 0, lane) : 0xffffffffu;
+    uint32_t hStart = h < G ? ssg_start_word(P, item0 + 2 * h - 1, 0, lane) : 0xffffffffu;
     while (done < total) {
-        while (h < G && off >= hStart + kWinPairs) {
+        while (h < G && off > hStart + kWinPairs) {
             ++h;
-            hStart = h < G ? ssg_start_word(P, item0 + h, 0, lane) : 0xffffffffu;
+            hStart = h < G ? ssg_start_word(P, item0 + 2 * h - 1, 0, lane) : 0xffffffffu;
         }
         if (h < G && off >= hStart) {
-            const uint32_t w = off - hStart;
-            const unsigned long long* bits = P.ssgBits + (size_t)(item0 + h) * kWinWords * 64 + lane;
-            if ((bits[(w / 64) * 64] >> (w % 64)) & 1ull) {
+            bool joined = false;
+            for (uint32_t ph = 0; ph < 2 && !joined; ++ph) {        // both phases of group h
+                const uint32_t it = item0 + 2 * h - 1 + ph;
+                if (off < hStart + ph) continue;
+                const uint32_t w = off - hStart - ph;
+                if (w >= kWinPairs) continue;
+                const unsigned long long* bits = P.ssgBits + (size_t)it * kWinWords * 64 + lane;
+                if (!((bits[(w / 64) * 64] >> (w % 64)) & 1ull)) continue;
                 uint32_t kh = __popcll(bits[(w / 64) * 64] & ((1ull << (w % 64)) - 1ull));
                 for (uint32_t j = 0; j < w / 64; ++j) kh += __popcll(bits[j * 64]);
-                const uint32_t ch = P.ssgCount[(size_t)(item0 + h) * 64 + lane];
-                if (kh < ch) {                                // continue in group h's log
-                    cur = h;
+                const uint32_t ch = P.ssgCount[(size_t)it * 64 + lane];
+                if (kh < ch) {                                // continue in this item's log
+                    inPatch = false;
+                    cur = 2 * h - 1 + ph;
                     k = kh;
-                    base = hStart;
+                    base = hStart + ph;
                     cnt = ch;
-                    ++h;
-                    hStart = h < G ? ssg_start_word(P, item0 + h, 0, lane) : 0xffffffffu;
+                    joined = true;
+                    prevRel = kh ? P.ssgEnd[((size_t)it * P.ssgCap + kh - 1) * 64 + lane] : 0u;
+                }
+            }
+            if (joined) {
+                ++h;
+                hStart = h < G ? ssg_start_word(P, item0 + 2 * h - 1, 0, lane) : 0xffffffffu;
+                continue;
+            }
+        }
+        if (k >= cnt && !inPatch && cur >= 2 && !(cur & 1u)) {
+            // a second-phase item ends where it joined its first phase: continue in that one's log
+            const uint32_t it = item0 + cur - 1;
+            const uint32_t w = off - (base - 1);
+            const unsigned long long* bits = P.ssgBits + (size_t)it * kWinWords * 64 + lane;
+            if (w < kWinPairs && ((bits[(w / 64) * 64] >> (w % 64)) & 1ull)) {
+                uint32_t kh = __popcll(bits[(w / 64) * 64] & ((1ull << (w % 64)) - 1ull));
+                for (uint32_t q = 0; q < w / 64; ++q) kh += __popcll(bits[q * 64]);
+                const uint32_t ch = P.ssgCount[(size_t)it * 64 + lane];
+                if (kh < ch) {
+                    cur -= 1;
+                    k = kh;
+                    base -= 1;
+                    cnt = ch;
+                    prevRel = kh ? P.ssgEnd[((size_t)it * P.ssgCap + kh - 1) * 64 + lane] : 0u;
                     continue;
                 }
             }
         }
         if (k >= cnt) break;
-        const size_t rec = (size_t)(item0 + cur) * P.ssgCap + k;
-        color = add(color, mk(P.ssgLog[(rec * 3 + 0) * 64 + lane], P.ssgLog[(rec * 3 + 1) * 64 + lane],
-                              P.ssgLog[(rec * 3 + 2) * 64 + lane]));
-        off = base + P.ssgEnd[rec * 64 + lane];
-        ++k;
-        ++done;
-        if (++sIdx == P.spp) {                                          // trace.cu:196
-            acc = (c == 0 && P.ignoreFirst) ? color : add(color, acc);
-            color = splat(0.0f);
-            sIdx = 0;
-            ++c;
+        // up to 16 samples at once (their loads issued together, the sums in order); the batch ends
+        // at the first sample start inside it that may be a junction or that passes group h's window,
+        // which the top of the loop then handles
+        uint32_t m = min(min(cnt - k, total - done), kFoldBatch);
+        const float* lg = inPatch ? patchLog : P.ssgLog;
+        const uint16_t* le = inPatch ? patchEnd : P.ssgEnd;
+        const size_t rec = inPatch ? (size_t)tile * patchCap + k : (size_t)(item0 + cur) * P.ssgCap + k;
+        float cx[kFoldBatch], cy[kFoldBatch], cz[kFoldBatch];
+        uint32_t er[kFoldBatch];
+#pragma unroll
+        for (uint32_t j = 0; j < kFoldBatch; ++j) {
+            if (j < m) {
+                cx[j] = lg[((rec + j) * 3 + 0) * 64 + lane];
+                cy[j] = lg[((rec + j) * 3 + 1) * 64 + lane];
+                cz[j] = lg[((rec + j) * 3 + 2) * 64 + lane];
+                er[j] = le[(rec + j) * 64 + lane];
+            }
         }
+        if (h < G && m > 1 && base + er[m - 2] >= hStart) {
+            // bit words of both phases around the batch's first start at or past hStart
+            const uint32_t p0 = max(base + er[0], hStart) - hStart;
+            const uint32_t i0 = min(p0 / 64, kWinWords - 1);
+            const unsigned long long* bA = P.ssgBits + (size_t)(item0 + 2 * h - 1) * kWinWords * 64 + lane;
+            const unsigned long long* bB = bA + (size_t)kWinWords * 64;
+            const unsigned long long a0 = bA[i0 * 64], a1 = i0 + 1 < kWinWords ? bA[(i0 + 1) * 64] : 0ull;
+            const uint32_t iB = p0 ? min((p0 - 1) / 64, kWinWords - 1) : 0u;
+            const unsigned long long c0 = bB[iB * 64], c1 = iB + 1 < kWinWords ? bB[(iB + 1) * 64] : 0ull;
+            auto bit = [&](unsigned long long w0, unsigned long long w1, uint32_t i, const unsigned long long* b,
+                           uint32_t w) -> bool {
+                const uint32_t idx = w / 64;
+                const unsigned long long word = idx == i ? w0 : (idx == i + 1 ? w1 : (idx < kWinWords ? b[idx * 64] : 0ull));
+                return (word >> (w % 64)) & 1ull;
+            };
+            for (uint32_t j = 0; j + 1 < m; ++j) {
+                const uint32_t pos = base + er[j];
+                if (pos < hStart) continue;
+                const uint32_t w = pos - hStart;
+                if (w > kWinPairs || (w < kWinPairs && bit(a0, a1, i0, bA, w)) || (w >= 1 && bit(c0, c1, iB, bB, w - 1))) {
+                    m = j + 1;
+                    break;
+                }
+            }
+        }
+        uint32_t endRel = prevRel;
+#pragma unroll
+        for (uint32_t j = 0; j < kFoldBatch; ++j) {
+            if (j < m) {
+                odd += (er[j] - endRel) & 1u;               // odd-length sample (guess statistics)
+                sq += (er[j] - endRel) * (er[j] - endRel);
+                endRel = er[j];
+            }
+        }
+        prevRel = endRel;
+#pragma unroll
+        for (uint32_t j = 0; j < kFoldBatch; ++j) {
+            if (j < m) {
+                color = add(color, mk(cx[j], cy[j], cz[j]));
+                if (++sIdx == P.spp) {                                  // trace.cu:196
+                    acc = (c == 0 && P.ignoreFirst) ? color : add(color, acc);
+                    color = splat(0.0f);
+                    sIdx = 0;
+                    ++c;
+                }
+            }
+        }
+        off = base + endRel;
+        k += m;
+        done += m;
     }
+    // the exact state at `off`: the current item's start state advanced by the draws since
     Xorwow st;
-    if (cur == 0) {
+    if (inPatch) {
+        st = {F[(F_ST + 0) * npix + li], F[(F_ST + 1) * npix + li], F[(F_ST + 2) * npix + li],
+              F[(F_ST + 3) * npix + li], F[(F_ST + 4) * npix + li], F[(F_ST + 5) * npix + li]};
+    } else if (cur == 0) {
         st = {P.rng[li], P.rng[npix + li], P.rng[2 * npix + li], P.rng[3 * npix + li], P.rng[4 * npix + li],
               P.rng[5 * npix + li]};
     } else {
@@ -1493,16 +1714,36 @@ __global__ void __launch_bounds__(256) ssg_fold_kernel(TraceParams P, uint32_t* 
     P.rng[4 * npix + li] = st.v3;
     P.rng[5 * npix + li] = st.v4;
     P.accum[li] = make_float4(acc.x, acc.y, acc.z, 1.0f);
-    if (done > 0) pairs[li] = (float)off / (float)done;
-    if (done < total) {
-        resume[li] = __float_as_uint(color.x);
-        resume[npix + li] = __float_as_uint(color.y);
-        resume[2 * npix + li] = __float_as_uint(color.z);
-        resume[3 * npix + li] = sIdx | (c << 16) | 0x80000000u;
-        atomicAdd(resumeCount, 1u);
-    } else {
-        resume[3 * npix + li] = 0u;
+    if (done == total) {
+        if (done > 0) {
+            pairs[li] = (float)off / (float)done;
+            pairs[npix + li] = (float)odd / (float)done;
+            const float mean = (float)off / (float)done;
+            pairs[2 * npix + li] = fmaxf((float)sq / (float)done - mean * mean, 0.0f);
+        }
+        F[F_FLAG * npix + li] = 0u;
+        return;
     }
+    F[(F_ACC + 0) * npix + li] = __float_as_uint(acc.x);
+    F[(F_ACC + 1) * npix + li] = __float_as_uint(acc.y);
+    F[(F_ACC + 2) * npix + li] = __float_as_uint(acc.z);
+    F[(F_COL + 0) * npix + li] = __float_as_uint(color.x);
+    F[(F_COL + 1) * npix + li] = __float_as_uint(color.y);
+    F[(F_COL + 2) * npix + li] = __float_as_uint(color.z);
+    F[F_SC * npix + li] = sIdx | (c << 16);
+    F[F_DONE * npix + li] = done;
+    F[F_OFF * npix + li] = off;
+    F[F_H * npix + li] = h;
+    F[F_ODD * npix + li] = odd;
+    F[F_SQ * npix + li] = sq;
+    F[(F_ST + 0) * npix + li] = st.d;
+    F[(F_ST + 1) * npix + li] = st.v0;
+    F[(F_ST + 2) * npix + li] = st.v1;
+    F[(F_ST + 3) * npix + li] = st.v2;
+    F[(F_ST + 4) * npix + li] = st.v3;
+    F[(F_ST + 5) * npix + li] = st.v4;
+    F[F_FLAG * npix + li] = 1u;
+    atomicAdd(deadCount, 1u);
 }
 
 // Multi-device gather, second half: scatter one device's received rows (its bands, in local row
@@ -1559,6 +1800,7 @@ struct pt_context {
     int schedule = 0;             // 0 = cost-sorted tiles (default), 1 = row-major
     // speculative sample groups
     int ssgMode = 0;              // 0 = automatic, 1 = off, G >= 2 = always G groups (tests)
+    uint32_t patchRounds = 6;     // patch rounds before the remaining dead ends run plain
     float* pairs = nullptr;       // per-pixel draw pairs per sample (start-offset guesses)
     bool pairsValid = false;
     uint32_t* ssgStart = nullptr;
@@ -1566,10 +1808,14 @@ struct pt_context {
     uint32_t* ssgCount = nullptr;
     float* ssgLog = nullptr;
     uint16_t* ssgEnd = nullptr;
-    uint32_t* resume = nullptr;   // [4][pixels]
-    uint32_t* resumeCount = nullptr;
-    size_t ssgItems = 0, ssgSamples = 0;   // allocated: items, and item x capacity sample records
+    uint32_t* fold = nullptr;     // [kFoldWords][pixels] fold state between rounds
+    uint32_t* deadCount = nullptr;
+    float* patchLog = nullptr;    // patch-round carriers: [tile][patchCap][3][64]
+    uint16_t* patchEnd = nullptr;
+    uint32_t* patchCount = nullptr;
+    size_t ssgItems = 0, ssgSamples = 0, patchSamples = 0;   // allocated capacities (records)
     uint32_t lastGroups = 0;      // groups of the last launch (0 = plain launch)
+    uint32_t groupStats[10] = {}; // G, patch rounds, dead-end pixels after fold rounds 0..7
     pt_camera lastCam = {};
     std::string err;
 };
@@ -1816,8 +2062,11 @@ PT_API void pt_destroy(pt_context* ctx)
     (void)hipFree(ctx->ssgCount);
     (void)hipFree(ctx->ssgLog);
     (void)hipFree(ctx->ssgEnd);
-    (void)hipFree(ctx->resume);
-    (void)hipFree(ctx->resumeCount);
+    (void)hipFree(ctx->fold);
+    (void)hipFree(ctx->deadCount);
+    (void)hipFree(ctx->patchLog);
+    (void)hipFree(ctx->patchEnd);
+    (void)hipFree(ctx->patchCount);
     for (auto& t : ctx->hostTex) (void)hipFree((void*)t.texels);
     if (ctx->ev0) (void)hipEventDestroy(ctx->ev0);
     if (ctx->ev1) (void)hipEventDestroy(ctx->ev1);
@@ -1978,9 +2227,9 @@ PT_API int pt_set_skybox(pt_context* ctx, uint32_t handle)
 }
 
 // Speculative sample groups: how many groups a launch uses (0 = a plain launch).  A launch of
-// `tiles` 8x8 tiles on a chip with `resident` wave slots runs the plain kernel while it has at least
-// four tiles per slot (the cost-sorted list schedule then balances); with fewer, each pixel's chain is
-// cut into enough groups for about six work items per slot, each group at least 32 samples long.
+// `tiles` 8x8 tiles on a chip with `resident` wave slots gets enough groups for about six work items
+// per slot (at most 8, each at least 64 samples long), and runs plain when that is fewer than 4
+// (1.5 tiles per slot or more: the cost-sorted list schedule balances well enough).
 static uint32_t ssg_groups(const pt_context* ctx, int variant, uint32_t tiles, uint32_t total)
 {
     if (ctx->ssgMode == 1 || (variant != 40 && variant != 41 && variant != 46)) return 0;
@@ -1988,21 +2237,25 @@ static uint32_t ssg_groups(const pt_context* ctx, int variant, uint32_t tiles, u
     int cus = 0;
     if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, ctx->device) != hipSuccess) return 0;
     const uint64_t resident = (uint64_t)cus * 4 * (variant == 46 ? 4 : 5);
-    if ((uint64_t)tiles >= 4 * resident) return 0;
     uint64_t g = (6 * resident + tiles - 1) / tiles;
-    g = std::min<uint64_t>({g, 16, total / 32});
-    return g >= 2 ? (uint32_t)g : 0;
+    g = std::min<uint64_t>({g, 8, total / 64});
+    // measured (tools/ssg_probe.py): with 2 or 3 groups the logging, the fold and the
+    // extra samples cost more than the shorter tail returns; from 4 groups on the tail wins
+    return g >= 4 ? (uint32_t)g : 0;
 }
 
 // Grow-only device buffers of the speculative groups; false if the device is out of memory (the
 // launch then runs plain).
-static bool ssg_reserve(pt_context* ctx, size_t items, size_t samples)
+static bool ssg_reserve(pt_context* ctx, size_t tiles, size_t items, size_t samples, size_t patchSamples)
 {
     const size_t npix = (size_t)ctx->rows * ctx->width;
+    auto fail_ = [] { (void)hipGetLastError(); return false; };
     if (!ctx->pairs) {
-        if (hipMalloc(&ctx->pairs, npix * sizeof(float)) != hipSuccess) return false;
-        if (hipMalloc(&ctx->resume, 4 * npix * sizeof(uint32_t)) != hipSuccess) return false;
-        if (hipMalloc(&ctx->resumeCount, sizeof(uint32_t)) != hipSuccess) return false;
+        if (hipMalloc(&ctx->pairs, 3 * npix * sizeof(float)) != hipSuccess ||
+            hipMalloc(&ctx->fold, kFoldWords * npix * sizeof(uint32_t)) != hipSuccess ||
+            hipMalloc(&ctx->deadCount, sizeof(uint32_t)) != hipSuccess ||
+            hipMalloc(&ctx->patchCount, tiles * 64 * sizeof(uint32_t)) != hipSuccess)
+            return fail_();
     }
     if (items > ctx->ssgItems) {
         (void)hipFree(ctx->ssgStart);
@@ -2012,12 +2265,10 @@ static bool ssg_reserve(pt_context* ctx, size_t items, size_t samples)
         ctx->ssgBits = nullptr;
         ctx->ssgCount = nullptr;
         ctx->ssgItems = 0;
-        if (hipMalloc(&ctx->ssgStart, items * 7 * 64 * sizeof(uint32_t)) != hipSuccess ||
+        if (hipMalloc(&ctx->ssgStart, items * kStartWords * 64 * sizeof(uint32_t)) != hipSuccess ||
             hipMalloc(&ctx->ssgBits, items * kWinWords * 64 * sizeof(unsigned long long)) != hipSuccess ||
-            hipMalloc(&ctx->ssgCount, items * 64 * sizeof(uint32_t)) != hipSuccess) {
-            (void)hipGetLastError();
-            return false;
-        }
+            hipMalloc(&ctx->ssgCount, items * 64 * sizeof(uint32_t)) != hipSuccess)
+            return fail_();
         ctx->ssgItems = items;
     }
     if (samples > ctx->ssgSamples) {
@@ -2027,11 +2278,20 @@ static bool ssg_reserve(pt_context* ctx, size_t items, size_t samples)
         ctx->ssgEnd = nullptr;
         ctx->ssgSamples = 0;
         if (hipMalloc(&ctx->ssgLog, samples * 64 * 3 * sizeof(float)) != hipSuccess ||
-            hipMalloc(&ctx->ssgEnd, samples * 64 * sizeof(uint16_t)) != hipSuccess) {
-            (void)hipGetLastError();
-            return false;
-        }
+            hipMalloc(&ctx->ssgEnd, samples * 64 * sizeof(uint16_t)) != hipSuccess)
+            return fail_();
         ctx->ssgSamples = samples;
+    }
+    if (patchSamples > ctx->patchSamples) {
+        (void)hipFree(ctx->patchLog);
+        (void)hipFree(ctx->patchEnd);
+        ctx->patchLog = nullptr;
+        ctx->patchEnd = nullptr;
+        ctx->patchSamples = 0;
+        if (hipMalloc(&ctx->patchLog, patchSamples * 64 * 3 * sizeof(float)) != hipSuccess ||
+            hipMalloc(&ctx->patchEnd, patchSamples * 64 * sizeof(uint16_t)) != hipSuccess)
+            return fail_();
+        ctx->patchSamples = patchSamples;
     }
     return true;
 }
@@ -2141,12 +2401,16 @@ static int render_impl(pt_context* ctx, const pt_camera* cam, uint32_t spp, uint
     uint32_t ssgN = 0, ssgCap = 0;
     if (G) {
         ssgN = total / G;
-        ssgCap = std::min<uint32_t>(total, ssgN + std::max<uint32_t>(512u, ssgN / 4));
-        ssgCap = std::min<uint32_t>(ssgCap, 10000u);       // end offsets are 16-bit draw pairs (<= 6 per sample)
-        const uint32_t lastN = total - (G - 1) * ssgN;
-        if (lastN > ssgCap || !ssg_reserve(ctx, (size_t)tiles * G, (size_t)tiles * G * ssgCap)) G = 0;
+        // an item runs its group and, where the next group's guess missed, into the group after it;
+        // further dead ends go to patch rounds
+        ssgCap = std::min<uint32_t>({total, 2 * ssgN + 64, 10000u});   // end offsets: 16-bit draw pairs (<= 6 per sample)
+        const size_t J = 2 * (size_t)G - 1;
+        if (!ssg_reserve(ctx, tiles, (size_t)tiles * J, (size_t)tiles * J * ssgCap, (size_t)tiles * ssgCap))
+            G = 0;
     }
     ctx->lastGroups = G;
+    memset(ctx->groupStats, 0, sizeof(ctx->groupStats));
+    ctx->groupStats[0] = G;
     PT_HIP_CHECK(ctx, hipEventRecord(ctx->ev0, ctx->stream));
     if (sorted && (ctx->orderStale || !ctx->orderValid) && (uint64_t)spp * chunks >= kPrepassMinSpp && !stats) {
         // Cold start (first launch, or the scene, a texture or the camera changed): a short cost
@@ -2170,34 +2434,58 @@ static int render_impl(pt_context* ctx, const pt_camera* cam, uint32_t spp, uint
         P.order = ctx->order;
     }
     if (G) {
-        const size_t items = (size_t)tiles * G;
+        const size_t items = (size_t)tiles * (2 * G - 1);
         const unsigned pixBlocks = (unsigned)(((size_t)tiles * 64 + 255) / 256);
         P.ssgG = G;
         P.ssgCap = ssgCap;
-        P.ssgLastN = total - (G - 1) * ssgN;
         P.ssgLog = ctx->ssgLog;
         P.ssgEnd = ctx->ssgEnd;
         P.ssgStart = ctx->ssgStart;
         P.ssgBits = ctx->ssgBits;
         P.ssgCount = ctx->ssgCount;
+        P.fold = ctx->fold;
         P.numSlots = (uint32_t)items;
         PT_HIP_CHECK(ctx, hipMemsetAsync(ctx->ssgBits, 0, items * kWinWords * 64 * sizeof(unsigned long long), ctx->stream));
-        PT_HIP_CHECK(ctx, hipMemsetAsync(ctx->resumeCount, 0, sizeof(uint32_t), ctx->stream));
+        PT_HIP_CHECK(ctx, hipMemsetAsync(ctx->deadCount, 0, sizeof(uint32_t), ctx->stream));
         if (P.tileCost) PT_HIP_CHECK(ctx, hipMemsetAsync(P.tileCost, 0, (size_t)tiles * sizeof(uint32_t), ctx->stream));
         ssg_guess_kernel<<<pixBlocks, 256, 0, ctx->stream>>>(P, ctx->pairsValid ? ctx->pairs : nullptr, ssgN, ctx->ssgStart);
         PT_HIP_CHECK(ctx, hipGetLastError());
         PT_HIP_CHECK(ctx, launch_grouped<1>(variant, P, ctx->stream));
-        ssg_fold_kernel<<<pixBlocks, 256, 0, ctx->stream>>>(P, ctx->resume, ctx->pairs, ctx->resumeCount);
+        ssg_fold_kernel<<<pixBlocks, 256, 0, ctx->stream>>>(P, 0, ctx->patchLog, ctx->patchEnd, ctx->patchCount, ssgCap,
+                                                             ctx->pairs, ctx->deadCount);
         PT_HIP_CHECK(ctx, hipGetLastError());
         ctx->pairsValid = true;
-        // the samples the logs did not cover (if any): the plain kernel from the fold's state
-        TraceParams R = P;
-        R.ssgG = 0;
-        R.numSlots = tiles;
-        R.order = nullptr;
-        R.tileCost = nullptr;
-        R.resume = ctx->resume;
-        PT_HIP_CHECK(ctx, launch_grouped<2>(variant, R, ctx->stream));
+        // Patch rounds: a carrier from each dead end (the exact state there) runs until it meets a
+        // later group's parse, and the fold continues; what is left after them runs plain.
+        TraceParams Q = P;
+        Q.ssgPatch = 1;
+        Q.ssgLog = ctx->patchLog;
+        Q.ssgEnd = ctx->patchEnd;
+        Q.ssgCount = ctx->patchCount;
+        Q.numSlots = tiles;
+        Q.order = nullptr;
+        Q.tileCost = nullptr;
+        uint32_t dead = 0;
+        for (uint32_t r = 1;; ++r) {
+            PT_HIP_CHECK(ctx, hipMemcpyAsync(&dead, ctx->deadCount, sizeof(uint32_t), hipMemcpyDeviceToHost, ctx->stream));
+            PT_HIP_CHECK(ctx, hipStreamSynchronize(ctx->stream));
+            if (r - 1 < 8) ctx->groupStats[2 + r - 1] = dead;
+            if (dead == 0 || r > ctx->patchRounds) break;
+            ctx->groupStats[1] = r;
+            PT_HIP_CHECK(ctx, hipMemsetAsync(ctx->deadCount, 0, sizeof(uint32_t), ctx->stream));
+            PT_HIP_CHECK(ctx, launch_grouped<1>(variant, Q, ctx->stream));
+            ssg_fold_kernel<<<pixBlocks, 256, 0, ctx->stream>>>(P, r, ctx->patchLog, ctx->patchEnd, ctx->patchCount, ssgCap,
+                                                                 ctx->pairs, ctx->deadCount);
+            PT_HIP_CHECK(ctx, hipGetLastError());
+        }
+        if (dead) {
+            TraceParams R = P;
+            R.ssgG = 0;
+            R.numSlots = tiles;
+            R.order = nullptr;
+            R.tileCost = nullptr;
+            PT_HIP_CHECK(ctx, launch_grouped<2>(variant, R, ctx->stream));
+        }
     } else {
         PT_HIP_CHECK(ctx, stats ? launch_variant<true>(variant, P, ctx->stream) : launch_variant<false>(variant, P, ctx->stream));
     }
@@ -2246,18 +2534,44 @@ PT_API int pt_set_sample_groups(pt_context* ctx, int mode)
     return PT_OK;
 }
 
+PT_API int pt_set_patch_rounds(pt_context* ctx, uint32_t rounds)
+{
+    if (!ctx || rounds > 64) return PT_ERR_ARG;
+    ctx->patchRounds = rounds;
+    return PT_OK;
+}
+
 PT_API int pt_last_sample_groups(const pt_context* ctx)
 {
     return ctx ? (int)ctx->lastGroups : 0;
 }
 
-PT_API int pt_read_resume_count(pt_context* ctx, uint32_t* count)
+PT_API int pt_read_group_log_counts(pt_context* ctx, uint32_t* dst, size_t count)
 {
-    if (!ctx || !count) return PT_ERR_ARG;
-    *count = 0;
-    if (!ctx->resumeCount || ctx->lastGroups == 0) return PT_OK;
+    if (!ctx || !dst) return PT_ERR_ARG;
+    if (!ctx->ssgCount || ctx->lastGroups == 0) return PT_ERR_STATE;
+    const size_t n = (size_t)((ctx->width + 7) / 8) * ((ctx->rows + 7) / 8) * (2 * ctx->lastGroups - 1) * 64;
+    if (count < n) return PT_ERR_ARG;
     PT_HIP_CHECK(ctx, hipSetDevice(ctx->device));
-    PT_HIP_CHECK(ctx, hipMemcpy(count, ctx->resumeCount, sizeof(uint32_t), hipMemcpyDeviceToHost));
+    PT_HIP_CHECK(ctx, hipMemcpy(dst, ctx->ssgCount, n * sizeof(uint32_t), hipMemcpyDeviceToHost));
+    return PT_OK;
+}
+
+PT_API int pt_read_group_fold(pt_context* ctx, uint32_t word, uint32_t* dst)
+{
+    if (!ctx || !dst || word >= kFoldWords + 1) return PT_ERR_ARG;
+    if (!ctx->fold) return PT_ERR_STATE;
+    PT_HIP_CHECK(ctx, hipSetDevice(ctx->device));
+    const size_t npix = (size_t)ctx->rows * ctx->width;
+    const void* src = word == kFoldWords ? (const void*)ctx->pairs : (const void*)(ctx->fold + (size_t)word * npix);
+    PT_HIP_CHECK(ctx, hipMemcpy(dst, src, npix * sizeof(uint32_t), hipMemcpyDeviceToHost));
+    return PT_OK;
+}
+
+PT_API int pt_read_group_stats(const pt_context* ctx, uint32_t* dst)
+{
+    if (!ctx || !dst) return PT_ERR_ARG;
+    memcpy(dst, ctx->groupStats, sizeof(ctx->groupStats));
     return PT_OK;
 }
 

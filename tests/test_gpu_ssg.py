@@ -53,10 +53,11 @@ def test_groups_bitexact_vs_oracle(gpu_available, scenes, name, W, H, spp, chunk
     assert np.array_equal(pt.rng_state(), ref.rng_array())
 
 
-def test_groups_equal_plain_launch_and_resume_path(gpu_available, scenes):
-    """One rank's share of the 1080p image at N = 8 (8-row bands): the automatic choice groups it; the
-    result equals the plain launch bit for bit.  Many groups over short chains force guesses that
-    miss, so the resume pass runs too."""
+@pytest.mark.parametrize("rounds", [6, 0])
+def test_groups_equal_plain_launch_patch_and_resume(gpu_available, scenes, rounds):
+    """One rank's share of the 1080p image at N = 8 (8-row bands): the automatic choice groups it, and
+    the result equals the plain launch bit for bit.  Many groups over short chains make guesses miss,
+    so patch rounds run (rounds = 6) or the plain resume launch takes the dead ends (rounds = 0)."""
     W, H = 1920, 1080
     p = str(scenes / "generated_scene.scene.json")
     out = {}
@@ -64,11 +65,15 @@ def test_groups_equal_plain_launch_and_resume_path(gpu_available, scenes):
         pt = pa.Pathtracer(W, H, row_offset=3, row_stride=8, band_rows=8)
         cam = pt.load_scene(p)
         pt.set_sample_groups(mode)
+        pt.set_patch_rounds(rounds)
         pt.render(cam, 8, True, chunks=32)
-        out[mode] = (pt.accum(), pt.rng_state(), pt.last_sample_groups, pt.resume_count())
+        out[mode] = (pt.accum(), pt.rng_state(), pt.last_sample_groups, pt.group_stats())
         pt.close()
     assert out[1][2] == 0 and out[0][2] >= 2 and out[16][2] == 16
     for mode in (0, 16):
         same(out[mode][0], out[1][0], f"mode {mode}")
         assert np.array_equal(out[mode][1], out[1][1])
-    assert out[16][3] > 0, "the resume pass was not exercised"
+    st = out[16][3]
+    assert st["dead_ends"][0] > 0, st                    # guesses missed somewhere: the later passes ran
+    if rounds:
+        assert st["patch_rounds"] >= 1, st

@@ -16,11 +16,17 @@ sys.path.insert(0, str(ROOT))
 import pathtracercuda_amd as pa  # noqa: E402
 
 
+SSG = 0
+GROUPS = {}
+
+
 def run(W, H, off, stride, band, spp, scene):
     pt = pa.Pathtracer(W, H, row_offset=off, row_stride=stride, band_rows=band)
+    pt.set_sample_groups(SSG)
     cam = pt.load_scene(scene)
-    pt.render_raw(cam, 8, 1, True)                       # records the tile costs -> sorted order
+    pt.render_raw(cam, 8, spp // 8, True)                # cold launch: cost order (+ draw-pair guesses)
     ms = pt.render_raw(cam, 8, spp // 8, True)
+    GROUPS[(stride, off)] = pt.last_sample_groups
     pt.close()
     return ms
 
@@ -33,9 +39,13 @@ def main():
     ap.add_argument("--height", type=int, default=2160)
     ap.add_argument("--scene", default=str(ROOT / "scenes/generated_scene.scene.json"))
     ap.add_argument("--partitions", default="rows:1,bands:8")
+    ap.add_argument("--ssg", type=int, default=0, help="speculative sample groups: 0 = automatic, 1 = off")
     a = ap.parse_args()
+    global SSG
+    SSG = a.ssg
     full = run(a.width, a.height, 0, 1, 1, a.spp, a.scene)
-    out = {"image": f"{a.width}x{a.height}", "spp": a.spp, "full_ms": round(full, 2), "partitions": {}}
+    out = {"image": f"{a.width}x{a.height}", "spp": a.spp, "ssg_mode": a.ssg, "full_ms": round(full, 2),
+           "full_groups": GROUPS.get((1, 0), 0), "partitions": {}}
     for part in a.partitions.split(","):
         name, band = part.split(":")
         res = {}
@@ -44,7 +54,7 @@ def main():
             worst = max(ranks)
             res[n] = {"rank_ms": [round(x, 2) for x in ranks], "rank_ms_max": round(worst, 2),
                       "ideal_ms": round(full / n, 2), "efficiency": round(full / n / worst, 3),
-                      "speedup": round(full / worst, 2)}
+                      "speedup": round(full / worst, 2), "groups": GROUPS.get((n, 0), 0)}
             print(json.dumps({name: {n: res[n]}}), flush=True)
         out["partitions"][name] = {"band_rows": int(band), "per_n": res}
     print(json.dumps(out))
