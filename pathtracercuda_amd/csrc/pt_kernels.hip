@@ -1908,6 +1908,8 @@ static hipError_t launch_one(const TraceParams& P, hipStream_t stream)
 //   40  default: resumable lean child-box walk, records in LDS, persistent waves, exit <= 24/64
 //   41  default for cache-read scenes: same, records through the caches, exit <= 12/64
 //   46  default for deep cache-read BVHs: variant 41 compiled for 4 waves/SIMD (128 VGPRs)
+//   47  small grids (<= 4 tiles per SIMD): variant 40 compiled for 4 waves/SIMD (128 VGPRs)
+//   48  small grids whose primitives fit in LDS too: variant 47 with records and primitives in LDS
 template <bool STATS, int MODE = 0>
 static hipError_t launch_variant(int v, const TraceParams& P, hipStream_t stream)
 {
@@ -1919,6 +1921,8 @@ static hipError_t launch_variant(int v, const TraceParams& P, hipStream_t stream
     case 40: return launch_one<STATS, 1, 4, 224, 5, true, MODE>(P, stream);
     case 41: return launch_one<STATS, 0, 4, 212, 5, true, MODE>(P, stream);
     case 46: return launch_one<STATS, 0, 4, 212, 4, true, MODE>(P, stream);
+    case 47: return launch_one<STATS, 1, 4, 224, 4, true, MODE>(P, stream);
+    case 48: return launch_one<STATS, 2, 4, 224, 4, true, MODE>(P, stream);
     default: return hipErrorInvalidValue;
     }
 }
@@ -1938,7 +1942,7 @@ static hipError_t launch_grouped(int v, const TraceParams& P, hipStream_t stream
 
 static bool variant_shipped(int v)
 {
-    return v == 0 || v == 1 || v == 4 || v == 6 || v == 20 || v == 40 || v == 41 || v == 46;
+    return v == 0 || v == 1 || v == 4 || v == 6 || v == 20 || v == 40 || v == 41 || v == 46 || v == 47 || v == 48;
 }
 
 // Cost pre-pass of a cold-start launch (render_impl): samples per pixel, and the smallest launch
@@ -2244,6 +2248,24 @@ static uint32_t ssg_groups(const pt_context* ctx, int variant, uint32_t tiles, u
     return g >= 4 ? (uint32_t)g : 0;
 }
 
+// A plain launch with at most four tiles per SIMD runs every tile in one pass at four waves per
+// SIMD, so the fifth wave slot the default kernels are compiled for (96 VGPRs, with spills) buys
+// nothing: the same walk compiled for four waves (128 VGPRs, no spill) shortens every wave's chain,
+// and when the primitives fit in LDS next to the child-box records, four workgroups per CU still
+// fit and leaf tests read LDS instead of L1/L2.  Measured (tools/ab_variants.py, MI355X): cornell
+// 512x512x64 +5.5 % (48), one rank's share of 1080p x 1024 at N = 8 +4 % (47).
+static int small_grid_variant(const pt_context* ctx, int variant, uint32_t tiles)
+{
+    int cus = 0;
+    if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, ctx->device) != hipSuccess) return variant;
+    if ((uint64_t)tiles > (uint64_t)cus * 4 * 4) return variant;
+    if (variant == 41) return 46;
+    if (variant != 40) return variant;
+    const size_t group = 4 * (size_t)ctx->cnodeCount * sizeof(float4) + 4 * (size_t)ctx->primCount * sizeof(float4) +
+                         4 * (size_t)ctx->stackDepth * 64 * 8 + 4 * 64 * 12;
+    return 4 * group <= 160 * 1024 ? 48 : 47;
+}
+
 // Grow-only device buffers of the speculative groups; false if the device is out of memory (the
 // launch then runs plain).
 static bool ssg_reserve(pt_context* ctx, size_t tiles, size_t items, size_t samples, size_t patchSamples)
@@ -2394,10 +2416,11 @@ static int render_impl(pt_context* ctx, const pt_camera* cam, uint32_t spp, uint
     P.tileCursor = ctx->tileCursor;
     P.numSlots = tiles;
     if (stats) PT_HIP_CHECK(ctx, hipMemsetAsync(ctx->stats, 0, 16 * sizeof(unsigned long long), ctx->stream));
-    const int variant = pick_variant(ctx);
+    int variant = pick_variant(ctx);
     // speculative sample groups
     const uint32_t total = spp * chunks;
     uint32_t G = (!stats && sorted && (uint64_t)spp * chunks < (1ull << 31)) ? ssg_groups(ctx, variant, tiles, total) : 0;
+    if (!G && ctx->variant == 0) variant = small_grid_variant(ctx, variant, tiles);
     uint32_t ssgN = 0, ssgCap = 0;
     if (G) {
         ssgN = total / G;

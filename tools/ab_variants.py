@@ -24,9 +24,14 @@ def main():
     ap.add_argument("--rounds", type=int, default=5)
     ap.add_argument("--variants", default="1,2,3,4,5")
     ap.add_argument("--schedules", default="0", help="tile schedules to cross with the variants (0 sorted, 1 row-major)")
+    ap.add_argument("--n", type=int, default=1, help="render one rank's share of an N-way 8-row band partition")
+    ap.add_argument("--rank", type=int, default=0)
+    ap.add_argument("--groups", type=int, default=1, help="sample groups: 1 = off (plain launches), 0 = automatic")
     a = ap.parse_args()
     vs = [(int(v), int(m)) for v in a.variants.split(",") for m in a.schedules.split(",")]
-    pt = pa.Pathtracer(a.width, a.height)
+    pt = (pa.Pathtracer(a.width, a.height, row_offset=a.rank, row_stride=a.n, band_rows=8) if a.n > 1
+          else pa.Pathtracer(a.width, a.height))
+    pt.set_sample_groups(a.groups)
     cam = pt.load_scene(a.scene)
     chunks = a.spp // 8
     ref = None
@@ -51,13 +56,14 @@ def main():
                 pt.render_raw(cam, 8, 1, True)     # records the tile costs for mode 0
             ms = pt.render_raw(cam, 8, chunks, True)
             times[(v, m)].append(ms)
-    samples = a.width * a.height * a.spp
+    samples = a.width * pt.rows * a.spp
     out = {}
     for v, m in vs:
         t = np.array(times[(v, m)])
         out[f"{v}" if len(a.schedules.split(",")) == 1 else f"{v}/s{m}"] = {"median_ms": float(np.median(t)), "min_ms": float(t.min()),
                   "Msamples_s": round(samples / (np.median(t) / 1e3) / 1e6, 1)}
-    print(json.dumps({"scene": pathlib.Path(a.scene).name, "spp": a.spp, "variants": out}))
+    print(json.dumps({"scene": pathlib.Path(a.scene).name, "image": f"{a.width}x{a.height}", "spp": a.spp,
+                      "n": a.n, "rank": a.rank, "variants": out}))
 
 
 if __name__ == "__main__":
