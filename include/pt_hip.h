@@ -196,7 +196,7 @@ PT_API int pt_set_schedule(pt_context *ctx, int mode);
  * 1 = never, G >= 2 = always G groups (tests).  pt_last_sample_groups: groups of the last launch
  * (0 = plain).  pt_read_group_stats fills 10 words: G, patch rounds run, and the pixels at a dead end
  * after fold rounds 0..7.  pt_read_group_log_counts: samples each (tile, item) logged per lane
- * ([tile][2G - 1][64], tiles row-major over the context; item 0 = group 0, items 2g - 1 and 2g =
+ * ([tile][2G - 1][64], tiles in dispatch (cost) order; item 0 = group 0, items 2g - 1 and 2g =
  * group g at its guessed offset and one draw pair later).  pt_set_patch_rounds: patch rounds before
  * the remaining dead ends run as a plain resume launch (default 6; 0 exercises the resume path). */
 PT_API int pt_set_sample_groups(pt_context *ctx, int mode);

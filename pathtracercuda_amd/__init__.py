@@ -282,8 +282,9 @@ class Pathtracer:
         return {"groups": v[0], "patch_rounds": v[1], "dead_ends": v[2:2 + v[1] + 1] if v[0] else []}
 
     def group_log_counts(self) -> np.ndarray:
-        """Samples each (tile, item) of the last grouped launch logged: (tiles, 2 * groups - 1, 64);
-        item 0 = group 0, items 2g - 1 and 2g = group g at its guess and one draw pair later."""
+        """Samples each (tile, item) of the last grouped launch logged: (tiles, 2 * groups - 1, 64), tiles
+        in dispatch (cost) order; item 0 = group 0, items 2g - 1 and 2g = group g at its guess and one
+        draw pair later."""
         g = 2 * self.last_sample_groups - 1
         tiles = ((self.width + 7) // 8) * ((self.rows + 7) // 8)
         out = np.zeros((tiles, g, 64), dtype=np.uint32)

@@ -84,15 +84,19 @@ struct TraceParams {
     // Speculative sample groups (0 = off).  A tile has J = 2G - 1 work items: item 0 =
     // group 0; items 2g - 1 and 2g = group g >= 1 started at its guessed draw offset and, for pixels
     // whose sample starts sit on the even lattice with rare odd shifts, one pair later (else that
-    // lane is idle).  Slot s runs tile order[s / J], item s % J; item index = tile * J + j.  Patch
-    // rounds (ssgPatch): one carrier per tile, lanes = the pixels the fold left at a dead end.
+    // lane is idle).  Slot s runs tile order[s / J], item s % J; item index = (s / J) * J + j, i.e. the
+    // per-item buffers are indexed by the tile's position in the order (ssgTiles = the grouped
+    // positions 0 .. ssgTiles - 1).  Patch rounds (ssgPatch):
+    // one carrier per grouped tile, lanes = the pixels the fold left at a dead end.
     uint32_t ssgG;              // groups per pixel
+    uint32_t ssgTiles;          // grouped tiles: order positions 0 .. ssgTiles - 1
     uint32_t ssgCap;            // sample-log capacity per item
     uint32_t ssgPatch;          // != 0: patch round
     float* ssgLog;              // [item][cap][3][64] path colours
     uint16_t* ssgEnd;           // [item][cap][64] end of each sample, in draw pairs from the item's start
     const uint32_t* ssgStart;   // [item][8][64] start offset (draw pairs; ~0 = idle lane), d, v0..v4, stop offset
-    unsigned long long* ssgBits;// [item][kWinWords][64] the item's sample starts in its window
+    unsigned long long* ssgBits;// [item][ssgWin][64] the item's sample starts in its window
+    uint32_t ssgWin;            // window words per lane (64 draw pairs each) after an item's start
     uint32_t* ssgCount;         // [item][64] samples logged
     uint32_t* fold;             // [kFoldWords][rows*width] fold state (ssg_fold_kernel); AUX resume input
     DevCamera cam;
@@ -100,8 +104,14 @@ struct TraceParams {
 
 // Speculative sample groups: window of a group's start offset in which an earlier group's parse can
 // join it (draw pairs; 16 x 64-bit words per lane), and the fold state kept per pixel between rounds.
-constexpr uint32_t kWinWords = 16;
-constexpr uint32_t kWinPairs = 64 * kWinWords;
+constexpr uint32_t kWinWords = 16;        // G >= 3: groups <= n samples apart, the window covers a group's start
+// With G = 2 the window covers the second group's whole range (up to 6 draw pairs per sample): in
+// long multi-bounce pixels two parses can take hundreds of samples to meet, and a first group that
+// never meets the second runs the whole chain (measured: every lane of a tile).
+static inline uint32_t ssg_window_words(uint32_t G, uint32_t n)
+{
+    return G == 2 ? (n * 6u + 256u + 63u) / 64u : kWinWords;
+}
 constexpr uint32_t kFoldBatch = 16;       // samples the fold loads at once
 constexpr uint32_t kStartWords = 8;       // start record: offset, d, v0..v4, stop offset (last group)
 enum : uint32_t { F_ACC = 0, F_COL = 3, F_SC = 6, F_DONE = 7, F_OFF = 8, F_H = 9, F_ST = 10, F_FLAG = 16, F_ODD = 17,
@@ -1054,8 +1064,8 @@ PT_DEV uint32_t wave_fetch(uint32_t* cursor, uint32_t n)
 // final state; whatever the logs do not cover runs in a resume launch.  Results are bit-identical.
 // ---------------------------------------------------------------------------------------------
 struct SsgLane {
-    uint32_t logItem;   // index into the log arrays: tile * J + j, or the tile in a patch round
-    uint32_t grp0;      // tile * J: the items of this tile
+    uint32_t logItem;   // index into the log arrays: pos * J + j, or pos in a patch round (pos: order position)
+    uint32_t grp0;      // pos * J: the items of this tile
     uint32_t g;         // group index; G in a patch round (no window of its own)
     uint32_t k;         // samples logged
     uint32_t d0;        // Weyl word at the item's start
@@ -1071,11 +1081,12 @@ PT_DEV uint32_t ssg_start_word(const TraceParams& P, uint32_t item, uint32_t w, 
     return P.ssgStart[((size_t)item * kStartWords + w) * 64 + lane];
 }
 
-PT_DEV void ssg_load(const TraceParams& P, uint32_t tile, uint32_t g, uint32_t lane, size_t li, size_t npix,
+// `pos`: the tile's position in the order (the per-item buffers' index), `g`: the item within it.
+PT_DEV void ssg_load(const TraceParams& P, uint32_t pos, uint32_t g, uint32_t lane, size_t li, size_t npix,
                      Xorwow& rng, PathState& ps, SsgLane& sl)
 {
     const uint32_t G = P.ssgG;
-    sl.grp0 = tile * (2 * G - 1);
+    sl.grp0 = pos * (2 * G - 1);
     sl.k = 0;
     ps.L = splat(0.0f);
     ps.T = splat(1.0f);
@@ -1083,7 +1094,7 @@ PT_DEV void ssg_load(const TraceParams& P, uint32_t tile, uint32_t g, uint32_t l
     if (P.ssgPatch) {
         // a carrier from the fold's dead end: the true state there, the fold's next candidate group
         const uint32_t* F = P.fold;
-        sl.logItem = tile;
+        sl.logItem = pos;
         sl.g = G;
         if (!(F[F_FLAG * npix + li] & 1u)) {       // finished pixel: its other fold words are stale
             sl.limit = 0;
@@ -1133,7 +1144,7 @@ PT_DEV void ssg_load(const TraceParams& P, uint32_t tile, uint32_t g, uint32_t l
             rng.v3 = ssg_start_word(P, sl.logItem, 5, lane);
             rng.v4 = ssg_start_word(P, sl.logItem, 6, lane);
             // the group's own start is its first sample start
-            __hip_atomic_fetch_or(&P.ssgBits[(size_t)sl.logItem * kWinWords * 64 + lane], 1ull, __ATOMIC_RELAXED,
+            __hip_atomic_fetch_or(&P.ssgBits[(size_t)sl.logItem * P.ssgWin * 64 + lane], 1ull, __ATOMIC_RELAXED,
                                   __HIP_MEMORY_SCOPE_AGENT);
         }
         sl.h = g + 1;
@@ -1161,20 +1172,20 @@ PT_DEV void ssg_finish(const TraceParams& P, PathState& ps, Xorwow& rng, float f
     P.ssgEnd[rec * 64 + lane] = (uint16_t)rel;
     ++sl.k;
     bool stop = sl.k >= sl.limit;
-    if (sl.g - 1u < P.ssgG - 1u && rel < kWinPairs)                    // groups 1 .. G-1
-        __hip_atomic_fetch_or(&P.ssgBits[((size_t)sl.logItem * kWinWords + rel / 64) * 64 + lane], 1ull << (rel % 64),
+    if (sl.g - 1u < P.ssgG - 1u && rel < (P.ssgWin * 64u))                    // groups 1 .. G-1
+        __hip_atomic_fetch_or(&P.ssgBits[((size_t)sl.logItem * P.ssgWin + rel / 64) * 64 + lane], 1ull << (rel % 64),
                               __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     const uint32_t off = sl.base + rel;
     stop = stop || off >= sl.stopOff;                                  // the last group: past the expected end
     const uint32_t j = sl.logItem - sl.grp0;
-    if (!stop && j >= 2 && !(j & 1u) && !P.ssgPatch && rel + 1 < kWinPairs) {
+    if (!stop && j >= 2 && !(j & 1u) && !P.ssgPatch && rel + 1 < (P.ssgWin * 64u)) {
         // the second phase has joined the first one's parse (a sample start of item j - 1): from here
         // the two are the same parse, the first carries on
         const uint32_t wa = rel + 1;
-        stop = (__hip_atomic_load(&P.ssgBits[((size_t)(sl.logItem - 1) * kWinWords + wa / 64) * 64 + lane], __ATOMIC_RELAXED,
+        stop = (__hip_atomic_load(&P.ssgBits[((size_t)(sl.logItem - 1) * P.ssgWin + wa / 64) * 64 + lane], __ATOMIC_RELAXED,
                                   __HIP_MEMORY_SCOPE_AGENT) >> (wa % 64)) & 1ull;
     }
-    while (sl.h < P.ssgG && off > sl.hStart + kWinPairs) {           // passed that group's windows
+    while (sl.h < P.ssgG && off > sl.hStart + (P.ssgWin * 64u)) {           // passed that group's windows
         ++sl.h;
         sl.hStart = sl.h < P.ssgG ? ssg_start_word(P, sl.grp0 + 2 * sl.h - 1, 0, lane) : 0xffffffffu;
     }
@@ -1182,11 +1193,11 @@ PT_DEV void ssg_finish(const TraceParams& P, PathState& ps, Xorwow& rng, float f
         // junction: a sample start of group h's parse (either phase; an idle phase has no bits)
         const uint32_t w = off - sl.hStart;
         const size_t itA = sl.grp0 + 2 * sl.h - 1;
-        if (w < kWinPairs)
-            stop = (__hip_atomic_load(&P.ssgBits[(itA * kWinWords + w / 64) * 64 + lane], __ATOMIC_RELAXED,
+        if (w < (P.ssgWin * 64u))
+            stop = (__hip_atomic_load(&P.ssgBits[(itA * P.ssgWin + w / 64) * 64 + lane], __ATOMIC_RELAXED,
                                       __HIP_MEMORY_SCOPE_AGENT) >> (w % 64)) & 1ull;
         if (!stop && w >= 1)
-            stop = (__hip_atomic_load(&P.ssgBits[((itA + 1) * kWinWords + (w - 1) / 64) * 64 + lane], __ATOMIC_RELAXED,
+            stop = (__hip_atomic_load(&P.ssgBits[((itA + 1) * P.ssgWin + (w - 1) / 64) * 64 + lane], __ATOMIC_RELAXED,
                                       __HIP_MEMORY_SCOPE_AGENT) >> ((w - 1) % 64)) & 1ull;
     }
     if (stop) {
@@ -1314,16 +1325,14 @@ __global__ void __launch_bounds__(WPB * 64, MINW) trace_kernel(TraceParams P)
     Counters cnt = {};
     uint32_t slot = PERSIST ? wave_fetch(P.tileCursor, 1u) : blockIdx.x * (uint32_t)WPB + wave;
     for (;;) {
-    if (PERSIST && slot >= P.numSlots) break;
-    uint32_t tile, grp = 0;
+    if (slot >= P.numSlots) break;               // also the grid's spare slots past the last item
+    uint32_t tile, grp = 0, pos = slot;              // pos: the tile's position in the order
     if (SSG && !P.ssgPatch) {
         const uint32_t J = 2 * P.ssgG - 1;
-        const uint32_t ts = slot / J;
-        grp = slot - ts * J;                         // item within the tile (ssg_load)
-        tile = P.order ? P.order[ts] : ts;
-    } else {
-        tile = P.order ? P.order[slot] : slot;
+        pos = slot / J;
+        grp = slot - pos * J;                        // item within the tile (ssg_load)
     }
+    tile = P.order ? P.order[pos] : pos;
     const PixelCtx pc = pixel_of(P, tile, lane);
     const uint64_t tWave = __builtin_amdgcn_s_memtime();
     const bool run = pc.valid && (!AUX || !P.fold || (P.fold[F_FLAG * pc.npix + pc.li] & 1u));
@@ -1331,7 +1340,7 @@ __global__ void __launch_bounds__(WPB * 64, MINW) trace_kernel(TraceParams P)
         Xorwow rng;
         PathState ps;
         SsgLane sl;
-        if (SSG) ssg_load(P, tile, grp, lane, pc.li, pc.npix, rng, ps, sl);
+        if (SSG) ssg_load(P, pos, grp, lane, pc.li, pc.npix, rng, ps, sl);
         else load_pixel<AUX>(P, pc, rng, ps, accL);
         const float fx = (float)(int32_t)pc.px, fy = (float)(int32_t)pc.py;
         camera_ray(P, fx, fy, rng, ps.o, ps.d);
@@ -1439,10 +1448,12 @@ __global__ void __launch_bounds__(256) tonemap_kernel(uchar4* out, const float4*
 // ---- speculative sample groups: start states and the fold ---------------------
 // Both run one lane per pixel, indexed like the trace kernel's items (tile, lane), so the per-item
 // buffers ([item][..][64]) are read and written in whole 256-B rows.
-PT_DEV bool ssg_pixel(const TraceParams& P, size_t gid, uint32_t& tile, uint32_t& lane, size_t& li)
+PT_DEV bool ssg_pixel(const TraceParams& P, size_t gid, uint32_t& pos, uint32_t& lane, size_t& li)
 {
-    tile = (uint32_t)(gid >> 6);
+    pos = (uint32_t)(gid >> 6);                      // position in the order: the per-item buffers' index
     lane = (uint32_t)(gid & 63u);
+    if (pos >= P.ssgTiles) return false;
+    const uint32_t tile = P.order ? P.order[pos] : pos;
     const uint32_t tileX = tile % P.tilesX, tileY = tile / P.tilesX;
     const uint32_t px = tileX * 8u + (lane & 7u), ly = tileY * 8u + (lane >> 3);
     li = (size_t)ly * P.width + px;
@@ -1572,7 +1583,7 @@ __global__ void __launch_bounds__(256) ssg_fold_kernel(TraceParams P, uint32_t r
     }
     uint32_t hStart = h < G ? ssg_start_word(P, item0 + 2 * h - 1, 0, lane) : 0xffffffffu;
     while (done < total) {
-        while (h < G && off > hStart + kWinPairs) {
+        while (h < G && off > hStart + (P.ssgWin * 64u)) {
             ++h;
             hStart = h < G ? ssg_start_word(P, item0 + 2 * h - 1, 0, lane) : 0xffffffffu;
         }
@@ -1582,8 +1593,8 @@ __global__ void __launch_bounds__(256) ssg_fold_kernel(TraceParams P, uint32_t r
                 const uint32_t it = item0 + 2 * h - 1 + ph;
                 if (off < hStart + ph) continue;
                 const uint32_t w = off - hStart - ph;
-                if (w >= kWinPairs) continue;
-                const unsigned long long* bits = P.ssgBits + (size_t)it * kWinWords * 64 + lane;
+                if (w >= (P.ssgWin * 64u)) continue;
+                const unsigned long long* bits = P.ssgBits + (size_t)it * P.ssgWin * 64 + lane;
                 if (!((bits[(w / 64) * 64] >> (w % 64)) & 1ull)) continue;
                 uint32_t kh = __popcll(bits[(w / 64) * 64] & ((1ull << (w % 64)) - 1ull));
                 for (uint32_t j = 0; j < w / 64; ++j) kh += __popcll(bits[j * 64]);
@@ -1608,8 +1619,8 @@ __global__ void __launch_bounds__(256) ssg_fold_kernel(TraceParams P, uint32_t r
             // a second-phase item ends where it joined its first phase: continue in that one's log
             const uint32_t it = item0 + cur - 1;
             const uint32_t w = off - (base - 1);
-            const unsigned long long* bits = P.ssgBits + (size_t)it * kWinWords * 64 + lane;
-            if (w < kWinPairs && ((bits[(w / 64) * 64] >> (w % 64)) & 1ull)) {
+            const unsigned long long* bits = P.ssgBits + (size_t)it * P.ssgWin * 64 + lane;
+            if (w < (P.ssgWin * 64u) && ((bits[(w / 64) * 64] >> (w % 64)) & 1ull)) {
                 uint32_t kh = __popcll(bits[(w / 64) * 64] & ((1ull << (w % 64)) - 1ull));
                 for (uint32_t q = 0; q < w / 64; ++q) kh += __popcll(bits[q * 64]);
                 const uint32_t ch = P.ssgCount[(size_t)it * 64 + lane];
@@ -1645,23 +1656,23 @@ __global__ void __launch_bounds__(256) ssg_fold_kernel(TraceParams P, uint32_t r
         if (h < G && m > 1 && base + er[m - 2] >= hStart) {
             // bit words of both phases around the batch's first start at or past hStart
             const uint32_t p0 = max(base + er[0], hStart) - hStart;
-            const uint32_t i0 = min(p0 / 64, kWinWords - 1);
-            const unsigned long long* bA = P.ssgBits + (size_t)(item0 + 2 * h - 1) * kWinWords * 64 + lane;
-            const unsigned long long* bB = bA + (size_t)kWinWords * 64;
-            const unsigned long long a0 = bA[i0 * 64], a1 = i0 + 1 < kWinWords ? bA[(i0 + 1) * 64] : 0ull;
-            const uint32_t iB = p0 ? min((p0 - 1) / 64, kWinWords - 1) : 0u;
-            const unsigned long long c0 = bB[iB * 64], c1 = iB + 1 < kWinWords ? bB[(iB + 1) * 64] : 0ull;
+            const uint32_t i0 = min(p0 / 64, P.ssgWin - 1);
+            const unsigned long long* bA = P.ssgBits + (size_t)(item0 + 2 * h - 1) * P.ssgWin * 64 + lane;
+            const unsigned long long* bB = bA + (size_t)P.ssgWin * 64;
+            const unsigned long long a0 = bA[i0 * 64], a1 = i0 + 1 < P.ssgWin ? bA[(i0 + 1) * 64] : 0ull;
+            const uint32_t iB = p0 ? min((p0 - 1) / 64, P.ssgWin - 1) : 0u;
+            const unsigned long long c0 = bB[iB * 64], c1 = iB + 1 < P.ssgWin ? bB[(iB + 1) * 64] : 0ull;
             auto bit = [&](unsigned long long w0, unsigned long long w1, uint32_t i, const unsigned long long* b,
                            uint32_t w) -> bool {
                 const uint32_t idx = w / 64;
-                const unsigned long long word = idx == i ? w0 : (idx == i + 1 ? w1 : (idx < kWinWords ? b[idx * 64] : 0ull));
+                const unsigned long long word = idx == i ? w0 : (idx == i + 1 ? w1 : (idx < P.ssgWin ? b[idx * 64] : 0ull));
                 return (word >> (w % 64)) & 1ull;
             };
             for (uint32_t j = 0; j + 1 < m; ++j) {
                 const uint32_t pos = base + er[j];
                 if (pos < hStart) continue;
                 const uint32_t w = pos - hStart;
-                if (w > kWinPairs || (w < kWinPairs && bit(a0, a1, i0, bA, w)) || (w >= 1 && bit(c0, c1, iB, bB, w - 1))) {
+                if (w > (P.ssgWin * 64u) || (w < (P.ssgWin * 64u) && bit(a0, a1, i0, bA, w)) || (w >= 1 && bit(c0, c1, iB, bB, w - 1))) {
                     m = j + 1;
                     break;
                 }
@@ -1724,6 +1735,7 @@ __global__ void __launch_bounds__(256) ssg_fold_kernel(TraceParams P, uint32_t r
         F[F_FLAG * npix + li] = 0u;
         return;
     }
+    if (done > 0) pairs[li] = (float)off / (float)done;   // the next launch's guess for this pixel
     F[(F_ACC + 0) * npix + li] = __float_as_uint(acc.x);
     F[(F_ACC + 1) * npix + li] = __float_as_uint(acc.y);
     F[(F_ACC + 2) * npix + li] = __float_as_uint(acc.z);
@@ -1814,6 +1826,7 @@ struct pt_context {
     uint16_t* patchEnd = nullptr;
     uint32_t* patchCount = nullptr;
     size_t ssgItems = 0, ssgSamples = 0, patchSamples = 0;   // allocated capacities (records)
+    size_t ssgBitsWords = 0;
     uint32_t lastGroups = 0;      // groups of the last launch (0 = plain launch)
     uint32_t groupStats[10] = {}; // G, patch rounds, dead-end pixels after fold rounds 0..7
     pt_camera lastCam = {};
@@ -2268,7 +2281,8 @@ static int small_grid_variant(const pt_context* ctx, int variant, uint32_t tiles
 
 // Grow-only device buffers of the speculative groups; false if the device is out of memory (the
 // launch then runs plain).
-static bool ssg_reserve(pt_context* ctx, size_t tiles, size_t items, size_t samples, size_t patchSamples)
+static bool ssg_reserve(pt_context* ctx, size_t tiles, size_t items, size_t samples, size_t patchSamples,
+                        size_t bitsWords = 0)
 {
     const size_t npix = (size_t)ctx->rows * ctx->width;
     auto fail_ = [] { (void)hipGetLastError(); return false; };
@@ -2278,20 +2292,30 @@ static bool ssg_reserve(pt_context* ctx, size_t tiles, size_t items, size_t samp
             hipMalloc(&ctx->deadCount, sizeof(uint32_t)) != hipSuccess ||
             hipMalloc(&ctx->patchCount, tiles * 64 * sizeof(uint32_t)) != hipSuccess)
             return fail_();
+        // guess statistics until a pre-pass or fold measures them: 2 pairs per sample, odd-length
+        // fraction unknown (< 0), variance 1
+        if (hipMemsetD32Async(reinterpret_cast<hipDeviceptr_t>(ctx->pairs), 0x40000000, npix, ctx->stream) != hipSuccess ||
+            hipMemsetD32Async(reinterpret_cast<hipDeviceptr_t>(ctx->pairs + npix), 0xbf800000, npix, ctx->stream) != hipSuccess ||
+            hipMemsetD32Async(reinterpret_cast<hipDeviceptr_t>(ctx->pairs + 2 * npix), 0x3f800000, npix, ctx->stream) != hipSuccess)
+            return fail_();
     }
     if (items > ctx->ssgItems) {
         (void)hipFree(ctx->ssgStart);
-        (void)hipFree(ctx->ssgBits);
         (void)hipFree(ctx->ssgCount);
         ctx->ssgStart = nullptr;
-        ctx->ssgBits = nullptr;
         ctx->ssgCount = nullptr;
         ctx->ssgItems = 0;
         if (hipMalloc(&ctx->ssgStart, items * kStartWords * 64 * sizeof(uint32_t)) != hipSuccess ||
-            hipMalloc(&ctx->ssgBits, items * kWinWords * 64 * sizeof(unsigned long long)) != hipSuccess ||
             hipMalloc(&ctx->ssgCount, items * 64 * sizeof(uint32_t)) != hipSuccess)
             return fail_();
         ctx->ssgItems = items;
+    }
+    if (bitsWords > ctx->ssgBitsWords) {           // [item][window words][64 lanes]
+        (void)hipFree(ctx->ssgBits);
+        ctx->ssgBits = nullptr;
+        ctx->ssgBitsWords = 0;
+        if (hipMalloc(&ctx->ssgBits, bitsWords * 64 * sizeof(unsigned long long)) != hipSuccess) return fail_();
+        ctx->ssgBitsWords = bitsWords;
     }
     if (samples > ctx->ssgSamples) {
         (void)hipFree(ctx->ssgLog);
@@ -2316,6 +2340,82 @@ static bool ssg_reserve(pt_context* ctx, size_t tiles, size_t items, size_t samp
         ctx->patchSamples = patchSamples;
     }
     return true;
+}
+
+// Stable radix sort of (cost, tile) pairs, descending, into the dispatch order: deterministic, ties
+// in tile order.
+static int sort_order(pt_context* ctx, uint32_t tiles)
+{
+    size_t bytes = ctx->sortTempBytes;
+    PT_HIP_CHECK(ctx, rocprim::radix_sort_pairs_desc(ctx->sortTemp, bytes, ctx->tileCost, ctx->sortKeys, ctx->tileIds,
+                                                     ctx->order, tiles, 0, 32, ctx->stream));
+    PT_HIP_CHECK(ctx, hipStreamSynchronize(ctx->stream));
+    ctx->orderValid = true;
+    ctx->orderStale = false;
+    return PT_OK;
+}
+
+// Guess, grouped launch, fold, patch rounds and resume of speculative sample groups over the first
+// `groupTiles` tiles of P.order (all tiles when P.order is null), on `s`.
+static int run_groups(pt_context* ctx, int variant, const TraceParams& P0, uint32_t G, uint32_t groupTiles,
+                      uint32_t ssgCap, hipStream_t s)
+{
+    TraceParams P = P0;
+    const uint32_t total = P.spp * P.chunks;
+    const uint32_t ssgN = total / G;
+    const size_t items = (size_t)groupTiles * (2 * G - 1);
+    const unsigned pixBlocks = (unsigned)(((size_t)groupTiles * 64 + 255) / 256);
+    P.ssgG = G;
+    P.ssgTiles = groupTiles;
+    P.ssgCap = ssgCap;
+    P.ssgLog = ctx->ssgLog;
+    P.ssgEnd = ctx->ssgEnd;
+    P.ssgStart = ctx->ssgStart;
+    P.ssgBits = ctx->ssgBits;
+    P.ssgCount = ctx->ssgCount;
+    P.ssgWin = ssg_window_words(G, ssgN);
+    P.fold = ctx->fold;
+    P.numSlots = (uint32_t)items;
+    ctx->groupStats[0] = G;
+    PT_HIP_CHECK(ctx, hipMemsetAsync(ctx->ssgBits, 0, items * P.ssgWin * 64 * sizeof(unsigned long long), s));
+    PT_HIP_CHECK(ctx, hipMemsetAsync(ctx->deadCount, 0, sizeof(uint32_t), s));
+    ssg_guess_kernel<<<pixBlocks, 256, 0, s>>>(P, ctx->pairs, ssgN, ctx->ssgStart);
+    PT_HIP_CHECK(ctx, hipGetLastError());
+    PT_HIP_CHECK(ctx, launch_grouped<1>(variant, P, s));
+    ssg_fold_kernel<<<pixBlocks, 256, 0, s>>>(P, 0, ctx->patchLog, ctx->patchEnd, ctx->patchCount, ssgCap, ctx->pairs,
+                                              ctx->deadCount);
+    PT_HIP_CHECK(ctx, hipGetLastError());
+    ctx->pairsValid = true;
+    // Patch rounds: a carrier from each dead end (the exact state there) runs until it meets a
+    // later group's parse, and the fold continues; what is left after them runs plain.
+    TraceParams Q = P;
+    Q.ssgPatch = 1;
+    Q.ssgLog = ctx->patchLog;
+    Q.ssgEnd = ctx->patchEnd;
+    Q.ssgCount = ctx->patchCount;
+    Q.numSlots = groupTiles;
+    Q.tileCost = nullptr;
+    uint32_t dead = 0;
+    for (uint32_t r = 1;; ++r) {
+        PT_HIP_CHECK(ctx, hipMemcpyAsync(&dead, ctx->deadCount, sizeof(uint32_t), hipMemcpyDeviceToHost, s));
+        PT_HIP_CHECK(ctx, hipStreamSynchronize(s));
+        if (r - 1 < 8) ctx->groupStats[2 + r - 1] = dead;
+        if (dead == 0 || r > ctx->patchRounds) break;
+        ctx->groupStats[1] = r;
+        PT_HIP_CHECK(ctx, hipMemsetAsync(ctx->deadCount, 0, sizeof(uint32_t), s));
+        PT_HIP_CHECK(ctx, launch_grouped<1>(variant, Q, s));
+        ssg_fold_kernel<<<pixBlocks, 256, 0, s>>>(P, r, ctx->patchLog, ctx->patchEnd, ctx->patchCount, ssgCap, ctx->pairs,
+                                                  ctx->deadCount);
+        PT_HIP_CHECK(ctx, hipGetLastError());
+    }
+    if (dead) {
+        TraceParams R = P;
+        R.ssgG = 0;
+        R.numSlots = groupTiles;
+        R.tileCost = nullptr;
+        PT_HIP_CHECK(ctx, launch_grouped<2>(variant, R, s));
+    }
+    return PT_OK;
 }
 
 static int render_impl(pt_context* ctx, const pt_camera* cam, uint32_t spp, uint32_t chunks, int ignore, float* gpu_ms,
@@ -2419,21 +2519,11 @@ static int render_impl(pt_context* ctx, const pt_camera* cam, uint32_t spp, uint
     int variant = pick_variant(ctx);
     // speculative sample groups
     const uint32_t total = spp * chunks;
-    uint32_t G = (!stats && sorted && (uint64_t)spp * chunks < (1ull << 31)) ? ssg_groups(ctx, variant, tiles, total) : 0;
+    const bool groupable = !stats && sorted && (uint64_t)spp * chunks < (1ull << 31);
+    uint32_t G = groupable ? ssg_groups(ctx, variant, tiles, total) : 0;
     if (!G && ctx->variant == 0) variant = small_grid_variant(ctx, variant, tiles);
-    uint32_t ssgN = 0, ssgCap = 0;
-    if (G) {
-        ssgN = total / G;
-        // an item runs its group and, where the next group's guess missed, into the group after it;
-        // further dead ends go to patch rounds
-        ssgCap = std::min<uint32_t>({total, 2 * ssgN + 64, 10000u});   // end offsets: 16-bit draw pairs (<= 6 per sample)
-        const size_t J = 2 * (size_t)G - 1;
-        if (!ssg_reserve(ctx, tiles, (size_t)tiles * J, (size_t)tiles * J * ssgCap, (size_t)tiles * ssgCap))
-            G = 0;
-    }
-    ctx->lastGroups = G;
+    ctx->lastGroups = 0;
     memset(ctx->groupStats, 0, sizeof(ctx->groupStats));
-    ctx->groupStats[0] = G;
     PT_HIP_CHECK(ctx, hipEventRecord(ctx->ev0, ctx->stream));
     if (sorted && (ctx->orderStale || !ctx->orderValid) && (uint64_t)spp * chunks >= kPrepassMinSpp && !stats) {
         // Cold start (first launch, or the scene, a texture or the camera changed): a short cost
@@ -2441,74 +2531,35 @@ static int render_impl(pt_context* ctx, const pt_camera* cam, uint32_t spp, uint
         // state, nothing written back (discard) -- and the launch below already runs in cost order.
         // Progressive 1-spp frames skip it and reuse the previous order for one launch instead.
         TraceParams Q = P;
-        Q.spp = G ? 8u : kPrepassSpp;              // speculative groups also take their offset guesses from it
+        const bool guesses = G != 0;           // speculative groups also take their offset guesses from it
+        Q.spp = guesses ? 8u : kPrepassSpp;
         Q.chunks = 1;
         Q.ignoreFirst = 1;
         Q.discard = 1;
         Q.order = nullptr;
-        Q.pairsOut = G ? ctx->pairs : nullptr;
-        if (G) ctx->pairsValid = true;
-        PT_HIP_CHECK(ctx, G ? launch_grouped<2>(variant, Q, ctx->stream) : launch_variant<false>(variant, Q, ctx->stream));
-        size_t bytes = ctx->sortTempBytes;
-        PT_HIP_CHECK(ctx, rocprim::radix_sort_pairs_desc(ctx->sortTemp, bytes, ctx->tileCost, ctx->sortKeys, ctx->tileIds,
-                                                         ctx->order, tiles, 0, 32, ctx->stream));
-        ctx->orderValid = true;
-        ctx->orderStale = false;
+        Q.pairsOut = guesses && ssg_reserve(ctx, tiles, 0, 0, 0) ? ctx->pairs : nullptr;
+        if (Q.pairsOut) ctx->pairsValid = true;
+        PT_HIP_CHECK(ctx, Q.pairsOut ? launch_grouped<2>(variant, Q, ctx->stream) : launch_variant<false>(variant, Q, ctx->stream));
+        const int rs = sort_order(ctx, tiles);
+        if (rs != PT_OK) return rs;
         P.order = ctx->order;
     }
+    uint32_t ssgCap = 0;
     if (G) {
-        const size_t items = (size_t)tiles * (2 * G - 1);
-        const unsigned pixBlocks = (unsigned)(((size_t)tiles * 64 + 255) / 256);
-        P.ssgG = G;
-        P.ssgCap = ssgCap;
-        P.ssgLog = ctx->ssgLog;
-        P.ssgEnd = ctx->ssgEnd;
-        P.ssgStart = ctx->ssgStart;
-        P.ssgBits = ctx->ssgBits;
-        P.ssgCount = ctx->ssgCount;
-        P.fold = ctx->fold;
-        P.numSlots = (uint32_t)items;
-        PT_HIP_CHECK(ctx, hipMemsetAsync(ctx->ssgBits, 0, items * kWinWords * 64 * sizeof(unsigned long long), ctx->stream));
-        PT_HIP_CHECK(ctx, hipMemsetAsync(ctx->deadCount, 0, sizeof(uint32_t), ctx->stream));
-        if (P.tileCost) PT_HIP_CHECK(ctx, hipMemsetAsync(P.tileCost, 0, (size_t)tiles * sizeof(uint32_t), ctx->stream));
-        ssg_guess_kernel<<<pixBlocks, 256, 0, ctx->stream>>>(P, ctx->pairsValid ? ctx->pairs : nullptr, ssgN, ctx->ssgStart);
-        PT_HIP_CHECK(ctx, hipGetLastError());
-        PT_HIP_CHECK(ctx, launch_grouped<1>(variant, P, ctx->stream));
-        ssg_fold_kernel<<<pixBlocks, 256, 0, ctx->stream>>>(P, 0, ctx->patchLog, ctx->patchEnd, ctx->patchCount, ssgCap,
-                                                             ctx->pairs, ctx->deadCount);
-        PT_HIP_CHECK(ctx, hipGetLastError());
-        ctx->pairsValid = true;
-        // Patch rounds: a carrier from each dead end (the exact state there) runs until it meets a
-        // later group's parse, and the fold continues; what is left after them runs plain.
-        TraceParams Q = P;
-        Q.ssgPatch = 1;
-        Q.ssgLog = ctx->patchLog;
-        Q.ssgEnd = ctx->patchEnd;
-        Q.ssgCount = ctx->patchCount;
-        Q.numSlots = tiles;
-        Q.order = nullptr;
-        Q.tileCost = nullptr;
-        uint32_t dead = 0;
-        for (uint32_t r = 1;; ++r) {
-            PT_HIP_CHECK(ctx, hipMemcpyAsync(&dead, ctx->deadCount, sizeof(uint32_t), hipMemcpyDeviceToHost, ctx->stream));
-            PT_HIP_CHECK(ctx, hipStreamSynchronize(ctx->stream));
-            if (r - 1 < 8) ctx->groupStats[2 + r - 1] = dead;
-            if (dead == 0 || r > ctx->patchRounds) break;
-            ctx->groupStats[1] = r;
-            PT_HIP_CHECK(ctx, hipMemsetAsync(ctx->deadCount, 0, sizeof(uint32_t), ctx->stream));
-            PT_HIP_CHECK(ctx, launch_grouped<1>(variant, Q, ctx->stream));
-            ssg_fold_kernel<<<pixBlocks, 256, 0, ctx->stream>>>(P, r, ctx->patchLog, ctx->patchEnd, ctx->patchCount, ssgCap,
-                                                                 ctx->pairs, ctx->deadCount);
-            PT_HIP_CHECK(ctx, hipGetLastError());
-        }
-        if (dead) {
-            TraceParams R = P;
-            R.ssgG = 0;
-            R.numSlots = tiles;
-            R.order = nullptr;
-            R.tileCost = nullptr;
-            PT_HIP_CHECK(ctx, launch_grouped<2>(variant, R, ctx->stream));
-        }
+        const uint32_t ssgN = total / G;
+        // an item runs its group and, where the next group's guess missed, into the group after it;
+        // further dead ends go to patch rounds
+        ssgCap = std::min<uint32_t>({total, 2 * ssgN + 64, 10000u});   // end offsets: 16-bit draw pairs (<= 6 per sample)
+        const size_t J = 2 * (size_t)G - 1;
+        if (!ssg_reserve(ctx, tiles, (size_t)tiles * J, (size_t)tiles * J * ssgCap, (size_t)tiles * ssgCap,
+                         (size_t)tiles * J * ssg_window_words(G, ssgN)))
+            G = 0;
+    }
+    if (G && P.tileCost) PT_HIP_CHECK(ctx, hipMemsetAsync(P.tileCost, 0, (size_t)tiles * sizeof(uint32_t), ctx->stream));
+    if (G) {
+        const int rc = run_groups(ctx, variant, P, G, tiles, ssgCap, ctx->stream);
+        if (rc != PT_OK) return rc;
+        ctx->lastGroups = G;
     } else {
         PT_HIP_CHECK(ctx, stats ? launch_variant<true>(variant, P, ctx->stream) : launch_variant<false>(variant, P, ctx->stream));
     }
@@ -2519,13 +2570,8 @@ static int render_impl(pt_context* ctx, const pt_camera* cam, uint32_t spp, uint
     PT_HIP_CHECK(ctx, hipEventElapsedTime(&ms, ctx->ev0, ctx->ev1));
     if (gpu_ms) *gpu_ms = ms;
     if (sorted && (ctx->orderStale || !ctx->orderValid)) {
-        // stable radix sort of (cost, tile) pairs, descending: deterministic, ties in tile order
-        size_t bytes = ctx->sortTempBytes;
-        PT_HIP_CHECK(ctx, rocprim::radix_sort_pairs_desc(ctx->sortTemp, bytes, ctx->tileCost, ctx->sortKeys, ctx->tileIds,
-                                                         ctx->order, tiles, 0, 32, ctx->stream));
-        PT_HIP_CHECK(ctx, hipStreamSynchronize(ctx->stream));
-        ctx->orderValid = true;
-        ctx->orderStale = false;
+        const int rs = sort_order(ctx, tiles);
+        if (rs != PT_OK) return rs;
     }
     if (stats) {
         unsigned long long h[16];
@@ -2568,6 +2614,7 @@ PT_API int pt_last_sample_groups(const pt_context* ctx)
 {
     return ctx ? (int)ctx->lastGroups : 0;
 }
+
 
 PT_API int pt_read_group_log_counts(pt_context* ctx, uint32_t* dst, size_t count)
 {

@@ -60,8 +60,9 @@ def main():
     out = {}
     for v, m in vs:
         t = np.array(times[(v, m)])
-        out[f"{v}" if len(a.schedules.split(",")) == 1 else f"{v}/s{m}"] = {"median_ms": float(np.median(t)), "min_ms": float(t.min()),
-                  "Msamples_s": round(samples / (np.median(t) / 1e3) / 1e6, 1)}
+        key = f"{v}" + ("" if len(a.schedules.split(",")) == 1 else f"/s{m}")
+        out[key] = {"median_ms": float(np.median(t)), "min_ms": float(t.min()),
+                    "Msamples_s": round(samples / (np.median(t) / 1e3) / 1e6, 1)}
     print(json.dumps({"scene": pathlib.Path(a.scene).name, "image": f"{a.width}x{a.height}", "spp": a.spp,
                       "n": a.n, "rank": a.rank, "variants": out}))
 
