@@ -190,6 +190,10 @@ class Run:
         self.pt.set_kernel_variant(20)
         st = self.pt.render_instrumented(self.cam, CHUNK, 1, True)
         self.pt.set_kernel_variant(0)
+        # the lane utilisation of the kernel that is timed: the same chunk with the default variant
+        # (its lanes run the same tests; only the wave schedule differs)
+        sd = self.pt.render_instrumented(self.cam, CHUNK, 1, True)
+        st.update({"d_" + k: v for k, v in sd.items() if k in LANE_KEYS})
         return st
 
     def step(self):
@@ -231,12 +235,18 @@ def timed(run, steps, warmup, local_rank, dist_on):
     return elapsed, kernel_ms
 
 
+LANE_KEYS = ("node_tests", "prim_tests", "hits", "sky_lookups", "segments", "wave_node_iters", "wave_prim_iters",
+             "wave_hits", "wave_sky")
+
+
 def lane_utilisation(st):
     """SIMD efficiency of each phase of the instrumented launch: lane-level events / (64 x wave-level
     executions).  An interior child-box visit counts two node tests per lane and one wave tick; the
     root test of each segment counts one of each."""
     def ratio(lanes, waves):
         return round(lanes / (64.0 * waves), 3) if waves else None
+    if "d_hits" in st:                     # the default kernel's instrumented chunk (Run.instrument)
+        st = {k: st["d_" + k] for k in LANE_KEYS}
     visits = (st["node_tests"] + st["segments"]) / 2.0
     return {"interior_walk": ratio(visits, st["wave_node_iters"]), "leaf_tests": ratio(st["prim_tests"], st["wave_prim_iters"]),
             "hit_shading": ratio(st["hits"], st["wave_hits"]), "sky_shading": ratio(st["sky_lookups"], st["wave_sky"])}
@@ -308,7 +318,7 @@ def main():
         if not dist_on:
             return st
         keys = ("node_tests", "prim_tests", "hits", "sky_lookups", "samples", "segments", "wave_node_iters",
-                "wave_prim_iters", "wave_hits", "wave_sky")
+                "wave_prim_iters", "wave_hits", "wave_sky") + tuple("d_" + k for k in LANE_KEYS if "d_" + k in st)
         t = torch.tensor([st[k] for k in keys], dtype=torch.float64, device=f"cuda:{local_rank}")
         dist.all_reduce(t)
         return dict(zip(keys, [float(x) for x in t]))

@@ -1347,13 +1347,36 @@ __global__ void __launch_bounds__(WPB * 64, MINW) trace_kernel(TraceParams P)
         uint64_t tAll = STATS ? __builtin_amdgcn_s_memtime() : 0;
         uint64_t tDone = 0;
         if (WW >= 100) {
-            bool fresh = true;
+            // DEFERQ (WW / 1000, eighths; 0 = off): a wave shades its pending hits only once they are at
+            // least DEFERQ/8 of its live lanes.  A lane whose hit is held back skips the traversal
+            // rounds until then (its closest hit stays in ts), so hit shading -- the longest branch
+            // -- runs for more lanes at once and in fewer rounds.  Every lane still performs its own
+            // sequence of operations in order; only the round in which it shades changes.
+            // SKYQ (WW / 10000): the same for misses (sky lookup, end of path, next camera ray).
+            // DEFERQ + SKYQ <= 8, so when every live lane is ready one class always runs.
+            constexpr int DEFERQ = (WW / 1000) % 10, SKYQ = (WW / 10000) % 10;
+            static_assert(DEFERQ + SKYQ <= 8, "a wave whose lanes are all ready must shade one class");
+            bool fresh = true, held = false;
             TravState ts = {0u, 0u, 0xffffffffu, kFltMax};
             while (ps.alive) {
-                if (STATS && fresh) { cnt.segments++; wave_tick(cnt.w_segments); }
-                const bool tdone = traverse_cb_phase<STATS, WW % 100>(nodes, prims, reinterpret_cast<uint2*>(stack), P,
-                                                                        ps.o, ps.d, fresh, ts, cnt);
-                fresh = tdone;
+                if (STATS && fresh && !held) { cnt.segments++; wave_tick(cnt.w_segments); }
+                bool tdone = true;
+                if (!held) {
+                    tdone = traverse_cb_phase<STATS, WW % 100>(nodes, prims, reinterpret_cast<uint2*>(stack), P, ps.o,
+                                                                ps.d, fresh, ts, cnt);
+                    fresh = tdone;
+                }
+                if (DEFERQ > 0 || SKYQ > 0) {
+                    const bool hitReady = tdone && ts.elem != 0xffffffffu;
+                    const bool missReady = tdone && ts.elem == 0xffffffffu;
+                    const uint32_t na = (uint32_t)__popcll(__ballot(1));
+                    bool hold = false;
+                    if (DEFERQ > 0) hold = hitReady && (uint32_t)__popcll(__ballot(hitReady)) * 8u < na * (uint32_t)DEFERQ;
+                    if (SKYQ > 0 && P.skybox != 0)     // without a sky texture a miss costs next to nothing
+                        hold = hold || (missReady && (uint32_t)__popcll(__ballot(missReady)) * 8u < na * (uint32_t)SKYQ);
+                    held = hold;
+                    if (held) continue;
+                }
                 if (!tdone) continue;                              // suspended: resumes next round
                 uint64_t tS = STATS ? __builtin_amdgcn_s_memtime() : 0;
                 if (shade<STATS>(P, prims, ts.elem, ts.tMax, ps, rng, cnt)) {
@@ -1931,11 +1954,12 @@ static hipError_t launch_variant(int v, const TraceParams& P, hipStream_t stream
     case 4: return launch_one<STATS, 0, 4, 1, 5, false, MODE>(P, stream);
     case 6: return launch_one<STATS, 1, 4, 1, 5, false, MODE>(P, stream);
     case 20: return launch_one<STATS, 0, 4, 3, 5, false, MODE>(P, stream);
-    case 40: return launch_one<STATS, 1, 4, 224, 5, true, MODE>(P, stream);
-    case 41: return launch_one<STATS, 0, 4, 212, 5, true, MODE>(P, stream);
-    case 46: return launch_one<STATS, 0, 4, 212, 4, true, MODE>(P, stream);
+    case 39: return launch_one<STATS, 1, 4, 224, 5, true, MODE>(P, stream);
+    case 40: return launch_one<STATS, 1, 4, 13216, 5, true, MODE>(P, stream);
+    case 41: return launch_one<STATS, 0, 4, 13212, 5, true, MODE>(P, stream);
+    case 46: return launch_one<STATS, 0, 4, 13212, 4, true, MODE>(P, stream);
     case 47: return launch_one<STATS, 1, 4, 224, 4, true, MODE>(P, stream);
-    case 48: return launch_one<STATS, 2, 4, 224, 4, true, MODE>(P, stream);
+    case 48: return launch_one<STATS, 2, 4, 13216, 4, true, MODE>(P, stream);
     default: return hipErrorInvalidValue;
     }
 }
@@ -1946,16 +1970,17 @@ template <int MODE>
 static hipError_t launch_grouped(int v, const TraceParams& P, hipStream_t stream)
 {
     switch (v) {
-    case 40: return launch_one<false, 1, 4, 224, 5, true, MODE>(P, stream);
-    case 41: return launch_one<false, 0, 4, 212, 5, true, MODE>(P, stream);
-    case 46: return launch_one<false, 0, 4, 212, 4, true, MODE>(P, stream);
+    case 39: return launch_one<false, 1, 4, 224, 5, true, MODE>(P, stream);
+    case 40: return launch_one<false, 1, 4, 13216, 5, true, MODE>(P, stream);
+    case 41: return launch_one<false, 0, 4, 13212, 5, true, MODE>(P, stream);
+    case 46: return launch_one<false, 0, 4, 13212, 4, true, MODE>(P, stream);
     default: return hipErrorInvalidValue;
     }
 }
 
 static bool variant_shipped(int v)
 {
-    return v == 0 || v == 1 || v == 4 || v == 6 || v == 20 || v == 40 || v == 41 || v == 46 || v == 47 || v == 48;
+    return v == 0 || v == 1 || v == 4 || v == 6 || v == 20 || v == 40 || v == 41 || v == 46 || v == 47 || v == 48 || v == 39;
 }
 
 // Cost pre-pass of a cold-start launch (render_impl): samples per pixel, and the smallest launch
@@ -2249,7 +2274,7 @@ PT_API int pt_set_skybox(pt_context* ctx, uint32_t handle)
 // (1.5 tiles per slot or more: the cost-sorted list schedule balances well enough).
 static uint32_t ssg_groups(const pt_context* ctx, int variant, uint32_t tiles, uint32_t total)
 {
-    if (ctx->ssgMode == 1 || (variant != 40 && variant != 41 && variant != 46)) return 0;
+    if (ctx->ssgMode == 1 || (variant != 39 && variant != 40 && variant != 41 && variant != 46)) return 0;
     if (ctx->ssgMode >= 2) return std::min<uint32_t>((uint32_t)ctx->ssgMode, std::max(total, 1u));
     int cus = 0;
     if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, ctx->device) != hipSuccess) return 0;
