@@ -1941,11 +1941,17 @@ static hipError_t launch_one(const TraceParams& P, hipStream_t stream)
 //   4   node-at-a-time while-while, caches, 5 waves/SIMD   (scenes outside the child-box encoding)
 //   6   node-at-a-time while-while, nodes in LDS           (idem, small BVH)
 //   20  child-box traversal, one tile per wave             (counts the reference's node/prim tests)
-//   40  default: resumable lean child-box walk, records in LDS, persistent waves, exit <= 24/64
+// The WW parameter of the resumable walk encodes 10000 * SKYQ + 1000 * DEFERQ + 200 + EXITQ
+// (deferred shading and the traversal's exit threshold, see trace_kernel).
+//   39  variant 40 without deferred shading, exit <= 24/64 (the round-1 default; A/B reference)
+//   40  default: resumable lean child-box walk, records in LDS, persistent waves, deferred shading
+//       (hits >= 3/8, misses >= 1/8 with a sky texture), exit <= 16/64
 //   41  default for cache-read scenes: same, records through the caches, exit <= 12/64
 //   46  default for deep cache-read BVHs: variant 41 compiled for 4 waves/SIMD (128 VGPRs)
-//   47  small grids (<= 4 tiles per SIMD): variant 40 compiled for 4 waves/SIMD (128 VGPRs)
-//   48  small grids whose primitives fit in LDS too: variant 47 with records and primitives in LDS
+//   47  small grids (<= 4 tiles per SIMD): variant 39 compiled for 4 waves/SIMD (128 VGPRs); no
+//       deferral, which costs a single pass of latency-bound waves 2.8 %
+//   48  small grids whose primitives fit in LDS too: records and primitives in LDS, 4 waves/SIMD,
+//       deferred hits
 template <bool STATS, int MODE = 0>
 static hipError_t launch_variant(int v, const TraceParams& P, hipStream_t stream)
 {
