@@ -2553,6 +2553,16 @@ static int render_impl(pt_context* ctx, const pt_camera* cam, uint32_t spp, uint
     const bool groupable = !stats && sorted && (uint64_t)spp * chunks < (1ull << 31);
     uint32_t G = groupable ? ssg_groups(ctx, variant, tiles, total) : 0;
     if (!G && ctx->variant == 0) variant = small_grid_variant(ctx, variant, tiles);
+    // Grouped launches of at most one tile per wave slot (one rank's 1080p share at N = 8) are
+    // short items whose latency sets the launch: deferred shading, which trades a lane's latency for
+    // fuller hit-shading rounds, measured bimodal there (median 57.7-62.6 ms against 57.8-58.2 ms
+    // without; at N = 4, two tiles per slot, 96.8 against 103.9), so they run the undeferred walk.
+    if (G && ctx->variant == 0 && variant == 40) {
+        int cus = 0;
+        if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, ctx->device) == hipSuccess &&
+            (uint64_t)tiles <= (uint64_t)cus * 4 * 5)
+            variant = 39;
+    }
     ctx->lastGroups = 0;
     memset(ctx->groupStats, 0, sizeof(ctx->groupStats));
     PT_HIP_CHECK(ctx, hipEventRecord(ctx->ev0, ctx->stream));

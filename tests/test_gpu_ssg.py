@@ -34,10 +34,12 @@ def same(a, b, what):
     ("generated_scene", 96, 54, 8, 16, 8),
     ("test_shapes", 80, 50, 8, 8, 3),
 ])
-def test_groups_bitexact_vs_oracle(gpu_available, scenes, name, W, H, spp, chunks, groups):
+@pytest.mark.parametrize("variant", [39, 40])          # grouped walk without / with deferred shading
+def test_groups_bitexact_vs_oracle(gpu_available, scenes, name, W, H, spp, chunks, groups, variant):
     p = scenes / f"{name}.scene.json"
     pt = pa.Pathtracer(W, H)
     cam = pt.load_scene(str(p))
+    pt.set_kernel_variant(variant)
     pt.set_sample_groups(groups)
     pt.render(cam, spp, True, chunks=chunks)
     assert pt.last_sample_groups == groups
