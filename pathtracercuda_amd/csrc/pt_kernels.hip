@@ -1952,6 +1952,9 @@ static hipError_t launch_one(const TraceParams& P, hipStream_t stream)
 //       deferral, which costs a single pass of latency-bound waves 2.8 %
 //   48  small grids whose primitives fit in LDS too: records and primitives in LDS, 4 waves/SIMD,
 //       deferred hits
+#ifndef PT_V40_WW
+#define PT_V40_WW 13216     // variant 40's walk parameters (A/B builds override it: tools/build_snap.sh)
+#endif
 template <bool STATS, int MODE = 0>
 static hipError_t launch_variant(int v, const TraceParams& P, hipStream_t stream)
 {
@@ -1961,7 +1964,7 @@ static hipError_t launch_variant(int v, const TraceParams& P, hipStream_t stream
     case 6: return launch_one<STATS, 1, 4, 1, 5, false, MODE>(P, stream);
     case 20: return launch_one<STATS, 0, 4, 3, 5, false, MODE>(P, stream);
     case 39: return launch_one<STATS, 1, 4, 224, 5, true, MODE>(P, stream);
-    case 40: return launch_one<STATS, 1, 4, 13216, 5, true, MODE>(P, stream);
+    case 40: return launch_one<STATS, 1, 4, PT_V40_WW, 5, true, MODE>(P, stream);
     case 41: return launch_one<STATS, 0, 4, 13212, 5, true, MODE>(P, stream);
     case 46: return launch_one<STATS, 0, 4, 13212, 4, true, MODE>(P, stream);
     case 47: return launch_one<STATS, 1, 4, 224, 4, true, MODE>(P, stream);
@@ -1977,7 +1980,7 @@ static hipError_t launch_grouped(int v, const TraceParams& P, hipStream_t stream
 {
     switch (v) {
     case 39: return launch_one<false, 1, 4, 224, 5, true, MODE>(P, stream);
-    case 40: return launch_one<false, 1, 4, 13216, 5, true, MODE>(P, stream);
+    case 40: return launch_one<false, 1, 4, PT_V40_WW, 5, true, MODE>(P, stream);
     case 41: return launch_one<false, 0, 4, 13212, 5, true, MODE>(P, stream);
     case 46: return launch_one<false, 0, 4, 13212, 4, true, MODE>(P, stream);
     default: return hipErrorInvalidValue;
