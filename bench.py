@@ -10,12 +10,19 @@ Every workload runs as the reference's headless loop renders it -- render() call
 tests/test_gpu_parity.py).  Inputs are resident on the GPU before the timed region (scene, BVH,
 sky texture, RNG state, accumulation buffer).
 
-N GPUs (torch.distributed.run, one process per GPU, RCCL): the image is cut into 8-row bands,
-band b -> rank b mod N (pathtracercuda_amd/distributed.py), each rank renders its bands and the HDR
-framebuffer is gathered to rank 0 over RCCL inside the timed region.  Default: strong scaling (the
+N GPUs, two launch modes, one partition (8-row bands, band b -> GPU b mod N):
+  * torch.distributed.run (WORLD_SIZE > 1, one process per GPU, RCCL): each rank renders its bands
+    and the HDR framebuffer is gathered to rank 0 over RCCL inside the timed region
+    (pathtracercuda_amd/distributed.py);
+  * `python bench.py --gpus N` without a launcher: the product's in-process multi-device Pathtracer
+    (pt_group_*: one context and host thread per GPU, ncclCommInitAll, grouped ncclSend/ncclRecv +
+    unpermute kernel -- the boundary that replaces Pathtracer.cpp:40's single device); the timed
+    step is pt_group_render + pt_group_gather.  Fewer than N visible GPUs is an error (exit 2);
+    `--group 1` runs this path at N = 1 too.  Default: strong scaling (the
 same workload for every N); `--scaling weak` grows the image by sqrt(N) per axis instead.  At N > 1
-a short weak-scaling measurement is added as a secondary field; at N = 1 the C2 workload is added
-as a secondary record (`--secondary 0` turns both off).
+a short weak-scaling measurement is added as a secondary field; at N = 1 the C2 and C5 workloads are
+added as secondary records, each with its roofline and CPU baseline (`--extra ''` drops C5,
+`--secondary 0` turns all of them off).
 
 Printed JSON line (rank 0): value = samples of the whole workload / step time.  roofline: the
 trace kernel is bound by VALU issue -- achieved = its wave64 VALU instructions per
@@ -56,7 +63,7 @@ CONFIGS = {
 }
 
 
-def parse_args():
+def parse_args(argv=None):
     p = argparse.ArgumentParser()
     p.add_argument("--gpus", type=int, default=1)
     p.add_argument("--steps", type=int, default=3)
@@ -70,7 +77,36 @@ def parse_args():
     p.add_argument("--cpu-baseline", type=int, default=1, help="time the oracle on a bounded sample (rank 0, N=1)")
     p.add_argument("--cpu-seconds", type=float, default=15.0, help="target length of the CPU baseline run")
     p.add_argument("--cpu-threads", type=int, default=0, help="0 = every core this process may use")
-    return p.parse_args()
+    p.add_argument("--extra", default="C5", help="N=1: secondary records after C2 (comma-separated labels; '' = none)")
+    p.add_argument("--group", type=int, default=-1,
+                   help="in-process device group (pt_group_*): 1 = always, 0 = never, -1 = when --gpus > 1 "
+                        "without a launcher")
+    return p.parse_args(argv)
+
+
+def resolve_mode(gpus: int, world: int, group: int, visible) -> str:
+    """Which path times the step: "torchrun" (one process per GPU, WORLD_SIZE > 1), "group" (this
+    process drives --gpus devices through pt_group_*), or "single".  `visible` is a callable giving
+    the number of visible GPUs (queried only for the group path).  Never silently runs fewer GPUs
+    than asked: a mismatch raises SystemExit(2) with the reason."""
+    if gpus < 1:
+        raise SystemExit("bench.py: --gpus must be >= 1")
+    if world > 1:
+        if gpus not in (1, world):
+            print(f"bench.py: --gpus {gpus} but WORLD_SIZE={world}", file=sys.stderr)
+            raise SystemExit(2)
+        return "torchrun"
+    if group == 0 and gpus > 1:
+        print(f"bench.py: --gpus {gpus} with --group 0 needs one process per GPU (torch.distributed.run "
+              f"--nproc-per-node {gpus})", file=sys.stderr)
+        raise SystemExit(2)
+    if gpus > 1 or group == 1:
+        n = int(visible())
+        if n < gpus:
+            print(f"bench.py: --gpus {gpus} but only {n} GPU(s) are visible", file=sys.stderr)
+            raise SystemExit(2)
+        return "group"
+    return "single"
 
 
 def scene_path(name: str) -> str:
@@ -160,22 +196,30 @@ def cpu_baseline(args, cfg, W, H):
 
 
 class Run:
-    """One workload on this rank: context, camera, gather buffers."""
+    """One workload on this rank: the renderer (one context, or the in-process device group), the
+    camera, the gather buffers of the torchrun path."""
 
-    def __init__(self, cfg, W, H, spp, rank, n, local_rank, band_rows, dist_on):
+    def __init__(self, cfg, W, H, spp, rank, n, local_rank, band_rows, mode):
         import torch
         import pathtracercuda_amd as pa
         from pathtracercuda_amd.distributed import global_rows, max_rows
 
         self.cfg, self.W, self.H, self.spp = cfg, W, H, spp
-        self.rank, self.n, self.dist_on = rank, n, dist_on
+        self.rank, self.n, self.mode = rank, n, mode
+        self.dist_on = mode == "torchrun"
         self.chunks = spp // CHUNK
         assert self.chunks * CHUNK == spp, "spp must be a multiple of 8"
-        self.band_rows = band_rows if dist_on else 1
-        self.pt = pa.Pathtracer(W, H, device=local_rank, row_offset=rank if dist_on else 0,
-                                row_stride=n if dist_on else 1, band_rows=self.band_rows)
+        self.band_rows = band_rows if mode != "single" else 1
+        self.gather_ms = 0.0
+        if mode == "group":
+            # the product's multi-device Pathtracer: one context per GPU, RCCL communicators from
+            # ncclCommInitAll, created before any other GPU work of this process
+            self.pt = pa.Pathtracer(W, H, devices=list(range(n)), band_rows=self.band_rows)
+        else:
+            self.pt = pa.Pathtracer(W, H, device=local_rank, row_offset=rank if self.dist_on else 0,
+                                    row_stride=n if self.dist_on else 1, band_rows=self.band_rows)
         self.cam = self.pt.load_scene(scene_path(cfg["scene"]))
-        if dist_on:
+        if self.dist_on:
             dev = f"cuda:{local_rank}"
             self.send = torch.zeros((max_rows(H, n, self.band_rows), W, 4), dtype=torch.float32, device=dev)
             self.recv = [torch.zeros_like(self.send) for _ in range(n)] if rank == 0 else None
@@ -186,19 +230,29 @@ class Run:
     def instrument(self):
         # one untimed 8-spp chunk with the non-speculative child-box kernel, whose node/primitive
         # tests are the reference's, for the algorithmic byte count and the lane utilisation; the
-        # launch also records the tile costs, so every timed launch runs in cost order
-        self.pt.set_kernel_variant(20)
-        st = self.pt.render_instrumented(self.cam, CHUNK, 1, True)
-        self.pt.set_kernel_variant(0)
+        # launch also records the tile costs, so every timed launch runs in cost order.  A device
+        # group counts on a one-device context of the whole image (the counts are per sample and do
+        # not depend on the partition); its own contexts get their cost order from the warm-up.
+        import pathtracercuda_amd as pa
+        pt = pa.Pathtracer(self.W, self.H, device=0) if self.mode == "group" else self.pt
+        cam = pt.load_scene(scene_path(self.cfg["scene"])) if self.mode == "group" else self.cam
+        pt.set_kernel_variant(20)
+        st = pt.render_instrumented(cam, CHUNK, 1, True)
+        pt.set_kernel_variant(0)
         # the lane utilisation of the kernel that is timed: the same chunk with the default variant
         # (its lanes run the same tests; only the wave schedule differs)
-        sd = self.pt.render_instrumented(self.cam, CHUNK, 1, True)
+        sd = pt.render_instrumented(cam, CHUNK, 1, True)
         st.update({"d_" + k: v for k, v in sd.items() if k in LANE_KEYS})
+        if self.mode == "group":
+            pt.close()
         return st
 
     def step(self):
         ms = self.pt.render_raw(self.cam, CHUNK, self.chunks, True)
-        if self.dist_on:
+        if self.mode == "group":
+            # RCCL gather of every device's bands to device 0 + unpermute (pt_group_gather)
+            self.gather_ms += self.pt.gather()
+        elif self.dist_on:
             from pathtracercuda_amd.distributed import gather_framebuffer
             # RCCL framebuffer gather over xGMI + scatter of the bands on rank 0
             self.pt.copy_accum_to_device(self.send.data_ptr(), self.send.numel() * 4)
@@ -214,14 +268,18 @@ def timed(run, steps, warmup, local_rank, dist_on):
     import torch
     import torch.distributed as dist
 
+    devices = range(run.n) if run.mode == "group" else [local_rank]
+
     def barrier_sync():
-        torch.cuda.synchronize(local_rank)
+        for d in devices:
+            torch.cuda.synchronize(d)
         if dist_on:
             dist.barrier()
 
     for _ in range(warmup):
         run.step()
     barrier_sync()
+    run.gather_ms = 0.0
     t0 = time.perf_counter()
     kernel_ms = 0.0
     for _ in range(steps):
@@ -296,20 +354,26 @@ def main():
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
-    if world == 1 and args.gpus > 1:
-        print(f"bench.py: --gpus {args.gpus} needs one process per GPU (torch.distributed.run "
-              f"--nproc-per-node {args.gpus}); running on 1 GPU", file=sys.stderr)
-    n = max(1, world)
+
+    def visible():
+        import pathtracercuda_amd as pa
+        return pa.device_count()
+
+    mode = resolve_mode(args.gpus, world, args.group, visible)
+    n = world if mode == "torchrun" else (args.gpus if mode == "group" else 1)
     cfg = CONFIGS[args.config]
     W, H, spp = cfg["width"], cfg["height"], args.spp or cfg["spp"]
     if args.scaling == "weak" and n > 1:
         W = int(round(W * math.sqrt(n) / 8.0)) * 8
         H = int(round(H * math.sqrt(n) / 8.0)) * 8
 
+    if mode == "group":
+        # the device group's communicators are created before torch touches any GPU
+        first = Run(cfg, W, H, spp, 0, n, 0, args.band_rows, mode)
     import torch
     import torch.distributed as dist
 
-    dist_on = world > 1
+    dist_on = mode == "torchrun"
     if dist_on:
         torch.cuda.set_device(local_rank)
         dist.init_process_group("nccl", device_id=torch.device("cuda", local_rank))
@@ -323,12 +387,15 @@ def main():
         dist.all_reduce(t)
         return dict(zip(keys, [float(x) for x in t]))
 
-    run = Run(cfg, W, H, spp, rank, n, local_rank, args.band_rows, dist_on)
+    run = first if mode == "group" else Run(cfg, W, H, spp, rank, n, local_rank, args.band_rows, mode)
     st = stats_all(run.instrument())
     elapsed, kernel_ms = timed(run, args.steps, args.warmup, local_rank, dist_on)
     main_rec = record(cfg, run, elapsed, kernel_ms, args.steps, st, n)
+    gather_ms = run.gather_ms
     run.close()
-    part = (f"{args.band_rows}-row bands interleaved x{n}, RCCL gather" if dist_on else "1 GPU")
+    part = {"torchrun": f"{args.band_rows}-row bands interleaved x{n}, one process per GPU, RCCL gather (torch.distributed)",
+            "group": f"{args.band_rows}-row bands interleaved x{n}, in-process device group (pt_group_*), RCCL gather",
+            "single": "1 GPU"}[mode]
     out = {
         "metric": METRIC,
         "value": main_rec["value"],
@@ -344,26 +411,33 @@ def main():
         "data": "synthetic sky (scenes/skybox.hdr); reference scene files (scenes/)",
         "config": {"workload": main_rec["workload"], "label": args.config, "scene": cfg["scene"], "width": W,
                    "height": H, "spp": spp, "render_calls_per_step": spp // CHUNK, "parallelism": part,
-                   "per_gpu_pixels": (W * H + n - 1) // n},
+                   "launch_mode": mode, "per_gpu_pixels": (W * H + n - 1) // n},
         "roofline": main_rec["roofline"],
         "cpu_baseline": None,
     }
+    if mode == "group":
+        out["group_timing"] = {"kernel_ms_per_step": round(kernel_ms / args.steps, 3),
+                               "gather_ms_per_step": round(gather_ms / args.steps, 3)}
     if args.secondary:
         if n == 1:
-            c2 = CONFIGS["C2"]
-            r2 = Run(c2, c2["width"], c2["height"], c2["spp"], 0, 1, local_rank, 1, False)
-            st2 = r2.instrument()
-            e2, k2 = timed(r2, max(args.steps, 5), args.warmup, local_rank, False)
-            rec2 = record(c2, r2, e2, k2, max(args.steps, 5), st2, 1)
-            r2.close()
-            rec2["label"] = "C2"
-            if rank == 0 and args.cpu_baseline:
-                rec2["cpu_baseline"] = cpu_baseline(args, c2, c2["width"], c2["height"])
-            out["secondary"] = [rec2]
+            recs = []
+            for label in ("C2",) + tuple(x for x in args.extra.split(",") if x):
+                c2 = CONFIGS[label]
+                r2 = Run(c2, c2["width"], c2["height"], c2["spp"], 0, 1, local_rank, 1, "single")
+                st2 = r2.instrument()
+                k2steps = max(args.steps, 5) if label == "C2" else args.steps
+                e2, k2 = timed(r2, k2steps, args.warmup, local_rank, False)
+                rec2 = record(c2, r2, e2, k2, k2steps, st2, 1)
+                r2.close()
+                rec2["label"] = label
+                if rank == 0 and args.cpu_baseline:
+                    rec2["cpu_baseline"] = cpu_baseline(args, c2, c2["width"], c2["height"])
+                recs.append(rec2)
+            out["secondary"] = recs
         elif args.scaling == "strong":
             Ww = int(round(cfg["width"] * math.sqrt(n) / 8.0)) * 8
             Hw = int(round(cfg["height"] * math.sqrt(n) / 8.0)) * 8
-            rw = Run(cfg, Ww, Hw, spp, rank, n, local_rank, args.band_rows, dist_on)
+            rw = Run(cfg, Ww, Hw, spp, rank, n, local_rank, args.band_rows, mode)
             stw = stats_all(rw.instrument())
             ew, kw = timed(rw, min(args.steps, 3), 1, local_rank, dist_on)
             recw = record(cfg, rw, ew, kw, min(args.steps, 3), stw, n)

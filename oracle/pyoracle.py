@@ -354,6 +354,19 @@ def rows_of(height: int, row_offset: int, row_stride: int, band_rows: int = 1) -
     return int(lib().or_view_rows(height, band_rows, row_offset, row_stride))
 
 
+def default_threads() -> int:
+    """Every CPU this process may use: the affinity mask, capped by the cgroup's CPU quota (the GPU
+    boxes show 256 logical CPUs but grant 16; more threads only time-slice them)."""
+    n = max(1, len(os.sched_getaffinity(0)))
+    try:
+        q, per = open("/sys/fs/cgroup/cpu.max").read().split()
+        if q != "max":
+            n = min(n, max(1, int(-(-float(q) // float(per)))))
+    except (OSError, ValueError):
+        pass
+    return n
+
+
 class OracleRenderer:
     """Per-pixel state of the reference Pathtracer (accum buffer, curandState, frame counter)
     restricted to the row bands b = row_offset + k * row_stride of band_rows rows (band_rows = 1:
@@ -369,7 +382,7 @@ class OracleRenderer:
         self.rng = (Xorwow * max(1, self.rows * width))()
         lib().or_init_rand_state(width, height, band_rows, row_offset, row_stride, self.rng)
         self.frames = 0
-        self.threads = threads or max(1, len(os.sched_getaffinity(0)))
+        self.threads = threads or default_threads()
         self.stats = np.zeros(7, dtype=np.uint64)
         self.fast = fast
 

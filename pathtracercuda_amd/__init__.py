@@ -142,13 +142,17 @@ class Pathtracer:
 
     Tiles: the image is cut into bands of `band_rows` rows and this object renders the bands
     b = row_offset + k * row_stride (band_rows = 1: rows y = row_offset + k * row_stride).
-    `devices=[...]` spans several GPUs of this process (pt_group_*, RCCL gather): the image calls
-    (accum, get_hdr_image_data, get_image_data) then return the full image.
+    `devices=[...]` spans several GPUs of this process (pt_group_*, RCCL gather; 8-row bands unless
+    `band_rows` says otherwise, as the C++ constructor and the CLI): the image calls (accum,
+    get_hdr_image_data, get_image_data, tonemap, rng_state) then cover the full image, the tuning
+    knobs apply to every device, and the per-context diagnostics raise PathtracerError.
     """
 
     def __init__(self, width: int, height: int, device: int = 0, row_offset: int = 0, row_stride: int = 1,
-                 band_rows: int = 1, devices: Optional[Sequence[int]] = None) -> None:
+                 band_rows: Optional[int] = None, devices: Optional[Sequence[int]] = None) -> None:
         self._r = C.c_void_p()
+        if band_rows is None:
+            band_rows = 8 if devices is not None else 1
         if devices is not None:
             devs = (C.c_int * len(devices))(*[int(d) for d in devices])
             N.check_host(N.host().pth_renderer_create_group(int(width), int(height), len(devices), devs, int(band_rows),
@@ -163,6 +167,29 @@ class Pathtracer:
         self.rows = int(N.host().pth_renderer_local_rows(self._r))
         self._ctx = N.host().pth_renderer_context(self._r)
         self._group = N.host().pth_renderer_group(self._r)
+
+    # --- device groups ------------------------------------------------------------------------
+    def _contexts(self):
+        """Every device context: the group's, or this object's one."""
+        if not self._group:
+            return [self._ctx]
+        return [N.hip().pt_group_context(self._group, i) for i in range(int(N.hip().pt_group_size(self._group)))]
+
+    def _single(self, what: str) -> None:
+        if self._group:
+            raise PathtracerError(N.PT_ERR_STATE, f"{what}: per-context call, not available on a device group "
+                                                  f"(use pt_group_context(i) through the C ABI)")
+
+    def _group_rows(self):
+        """Per device of a group: (context, its local rows' global row indices)."""
+        out = []
+        n = len(self.devices)
+        shift = self.band_rows.bit_length() - 1
+        for i, c in enumerate(self._contexts()):
+            rows = int(N.hip().pt_local_rows(c))
+            ly = np.arange(rows, dtype=np.int64)
+            out.append((c, ((i + (ly >> shift) * n) << shift) + (ly & (self.band_rows - 1))))
+        return out
 
     def close(self) -> None:
         if getattr(self, "_r", None):
@@ -225,22 +252,40 @@ class Pathtracer:
 
     def rng_state(self) -> np.ndarray:
         out = np.zeros((self.rows, self.width, 6), dtype=np.uint32)
+        if self._group:
+            for c, gy in self._group_rows():
+                part = np.zeros((gy.size, self.width, 6), dtype=np.uint32)
+                N.check_ctx(N.hip().pt_read_rng(c, part.ctypes.data_as(C.POINTER(C.c_uint32))), c)
+                out[gy] = part
+            return out
         N.check_ctx(N.hip().pt_read_rng(self._ctx, out.ctypes.data_as(C.POINTER(C.c_uint32))), self._ctx)
         return out
 
     def set_rng_state(self, state: np.ndarray) -> None:
         s = np.ascontiguousarray(state, dtype=np.uint32)
-        assert s.shape == (self.rows, self.width, 6)
+        if s.shape != (self.rows, self.width, 6):
+            raise PathtracerError(N.PT_ERR_ARG, f"set_rng_state: shape {s.shape}, expected {(self.rows, self.width, 6)}")
+        if self._group:
+            for c, gy in self._group_rows():
+                part = np.ascontiguousarray(s[gy])
+                N.check_ctx(N.hip().pt_write_rng(c, part.ctypes.data_as(C.POINTER(C.c_uint32))), c)
+            return
         N.check_ctx(N.hip().pt_write_rng(self._ctx, s.ctypes.data_as(C.POINTER(C.c_uint32))), self._ctx)
 
     def render_raw(self, camera: PtCamera, spp: int, chunks: int, ignore_history: bool) -> float:
-        """Device-layer launch without frame accounting; returns the kernel time in ms."""
+        """Device-layer launch without frame accounting; returns the kernel time in ms (a group: every
+        device concurrently, the slowest device's time; the next image read gathers again)."""
         ms = C.c_float(0.0)
+        if self._group:
+            N.check_group(N.hip().pt_group_render(self._group, C.byref(camera), int(spp), int(chunks),
+                                                  int(bool(ignore_history)), C.byref(ms)), self._group)
+            return float(ms.value)
         N.check_ctx(N.hip().pt_render(self._ctx, C.byref(camera), int(spp), int(chunks), int(bool(ignore_history)),
                                       C.byref(ms)), self._ctx)
         return float(ms.value)
 
     def render_instrumented(self, camera: PtCamera, spp: int, chunks: int, ignore_history: bool) -> Dict[str, int]:
+        self._single("render_instrumented")
         ms = C.c_float(0.0)
         st = PtRenderStats()
         N.check_ctx(N.hip().pt_render_instrumented(self._ctx, C.byref(camera), int(spp), int(chunks),
@@ -250,32 +295,40 @@ class Pathtracer:
         return d
 
     def set_kernel_variant(self, variant: int) -> None:
-        N.check_ctx(N.hip().pt_set_kernel_variant(self._ctx, int(variant)), self._ctx)
+        """pt_set_kernel_variant on every device context."""
+        for c in self._contexts():
+            N.check_ctx(N.hip().pt_set_kernel_variant(c, int(variant)), c)
 
     def set_schedule(self, mode: int) -> None:
-        """0 = cost-sorted tile dispatch (default), 1 = row-major (pt_set_schedule)."""
-        N.check_ctx(N.hip().pt_set_schedule(self._ctx, int(mode)), self._ctx)
+        """0 = cost-sorted tile dispatch (default), 1 = row-major (pt_set_schedule), every device."""
+        for c in self._contexts():
+            N.check_ctx(N.hip().pt_set_schedule(c, int(mode)), c)
 
     def set_sample_groups(self, mode: int) -> None:
         """Speculative sample groups (pt_set_sample_groups): 0 = automatic, 1 = off, G >= 2 = always G."""
-        N.check_ctx(N.hip().pt_set_sample_groups(self._ctx, int(mode)), self._ctx)
+        for c in self._contexts():
+            N.check_ctx(N.hip().pt_set_sample_groups(c, int(mode)), c)
 
     @property
     def last_sample_groups(self) -> int:
-        return int(N.hip().pt_last_sample_groups(self._ctx))
+        """Groups of the last launch (a device group: the largest over its devices)."""
+        return max(int(N.hip().pt_last_sample_groups(c)) for c in self._contexts())
 
     def set_patch_rounds(self, rounds: int) -> None:
-        N.check_ctx(N.hip().pt_set_patch_rounds(self._ctx, int(rounds)), self._ctx)
+        for c in self._contexts():
+            N.check_ctx(N.hip().pt_set_patch_rounds(c, int(rounds)), c)
 
     def group_fold_word(self, word: int) -> np.ndarray:
         """Diagnostics: a plane of the grouped launch's fold state (pt_read_group_fold); word 19 =
         draw pairs per sample (float32)."""
+        self._single("group_fold_word")
         out = np.zeros((self.rows, self.width), dtype=np.uint32)
         N.check_ctx(N.hip().pt_read_group_fold(self._ctx, int(word), out.ctypes.data_as(C.POINTER(C.c_uint32))), self._ctx)
         return out.view(np.float32) if word == 19 else out
 
     def group_stats(self) -> Dict[str, object]:
         """How the last grouped launch went: groups, patch rounds, dead-end pixels after each fold."""
+        self._single("group_stats")
         out = (C.c_uint32 * 10)()
         N.check_ctx(N.hip().pt_read_group_stats(self._ctx, out), self._ctx)
         v = list(out)
@@ -285,6 +338,7 @@ class Pathtracer:
         """Samples each (tile, item) of the last grouped launch logged: (tiles, 2 * groups - 1, 64), tiles
         in dispatch (cost) order; item 0 = group 0, items 2g - 1 and 2g = group g at its guess and one
         draw pair later."""
+        self._single("group_log_counts")
         g = 2 * self.last_sample_groups - 1
         tiles = ((self.width + 7) // 8) * ((self.rows + 7) // 8)
         out = np.zeros((tiles, g, 64), dtype=np.uint32)
@@ -294,21 +348,27 @@ class Pathtracer:
 
     def tile_costs(self) -> np.ndarray:
         """Shader-clock cycles of each 8x8 tile in the last launch (tiles_y x tiles_x)."""
+        self._single("tile_costs")
         tx, ty = (self.width + 7) // 8, (self.rows + 7) // 8
         out = np.zeros(tx * ty, dtype=np.uint32)
         N.check_ctx(N.hip().pt_read_tile_costs(self._ctx, out.ctypes.data_as(C.POINTER(C.c_uint32)), tx * ty), self._ctx)
         return out.reshape(ty, tx)
 
     def copy_accum_to_device(self, dst_ptr: int, nbytes: int) -> None:
+        self._single("copy_accum_to_device")
         N.check_ctx(N.hip().pt_copy_accum_device(self._ctx, C.c_void_p(int(dst_ptr)), int(nbytes)), self._ctx)
 
     def tonemap_device(self, dst_ptr: int, nbytes: int, frames: Optional[int] = None) -> None:
         """Tonemap into a device buffer (RGBA8, rows x width) -- the pixel-buffer path of render()."""
+        self._single("tonemap_device")
         f = self.frames if frames is None else int(frames)
         N.check_ctx(N.hip().pt_tonemap_device(self._ctx, f, C.c_void_p(int(dst_ptr)), int(nbytes)), self._ctx)
 
     def tonemap(self, frames: Optional[int] = None) -> np.ndarray:
         out = np.zeros((self.rows, self.width, 4), dtype=np.uint8)
         f = self.frames if frames is None else int(frames)
+        if self._group:
+            N.check_group(N.hip().pt_group_tonemap(self._group, f, out.ctypes.data_as(C.POINTER(C.c_uint8))), self._group)
+            return out
         N.check_ctx(N.hip().pt_tonemap(self._ctx, f, out.ctypes.data_as(C.POINTER(C.c_uint8))), self._ctx)
         return out

@@ -1853,6 +1853,7 @@ struct pt_context {
     uint32_t lastGroups = 0;      // groups of the last launch (0 = plain launch)
     uint32_t groupStats[10] = {}; // G, patch rounds, dead-end pixels after fold rounds 0..7
     pt_camera lastCam = {};
+    uint64_t epoch = 0;           // launches that wrote the accumulation (a group's gather cache key)
     std::string err;
 };
 
@@ -2553,7 +2554,8 @@ static int render_impl(pt_context* ctx, const pt_camera* cam, uint32_t spp, uint
     int variant = pick_variant(ctx);
     // speculative sample groups
     const uint32_t total = spp * chunks;
-    const bool groupable = !stats && sorted && (uint64_t)spp * chunks < (1ull << 31);
+    // the fold state packs (sample in call, call) into one word as sIdx | c << 16 (ssg_fold_kernel)
+    const bool groupable = !stats && sorted && (uint64_t)spp * chunks < (1ull << 31) && spp <= 0xffffu && chunks <= 0xffffu;
     uint32_t G = groupable ? ssg_groups(ctx, variant, tiles, total) : 0;
     if (!G && ctx->variant == 0) variant = small_grid_variant(ctx, variant, tiles);
     // Grouped launches of at most one tile per wave slot (one rank's 1080p share at N = 8) are
@@ -2568,6 +2570,7 @@ static int render_impl(pt_context* ctx, const pt_camera* cam, uint32_t spp, uint
     }
     ctx->lastGroups = 0;
     memset(ctx->groupStats, 0, sizeof(ctx->groupStats));
+    ++ctx->epoch;
     PT_HIP_CHECK(ctx, hipEventRecord(ctx->ev0, ctx->stream));
     if (sorted && (ctx->orderStale || !ctx->orderValid) && (uint64_t)spp * chunks >= kPrepassMinSpp && !stats) {
         // Cold start (first launch, or the scene, a texture or the camera changed): a short cost
@@ -2824,9 +2827,19 @@ struct pt_group {
     float4* stage = nullptr;          // device 0: the received rows of every device, concatenated
     float4* full = nullptr;           // device 0: the assembled image, height x width
     uchar4* ldr = nullptr;            // device 0: tonemap staging
-    bool gathered = false;            // `full` holds the current accumulation
+    // `full` holds the accumulation as of these context epochs (every launch on a context, through
+    // the group or directly on pt_group_context(i), bumps its epoch and so invalidates `full`)
+    std::vector<uint64_t> gatherEpoch;
     std::string err;
 };
+
+static bool group_gathered(const pt_group* g)
+{
+    if (g->gatherEpoch.size() != g->ctx.size()) return false;
+    for (size_t i = 0; i < g->ctx.size(); ++i)
+        if (g->gatherEpoch[i] != g->ctx[i]->epoch) return false;
+    return true;
+}
 
 static int gfail(pt_group* g, int code, const std::string& msg)
 {
@@ -2955,7 +2968,6 @@ PT_API int pt_group_render(pt_group* g, const pt_camera* camera, uint32_t spp, u
         for (size_t i = 0; i < n; ++i) th.emplace_back(one, i);
         for (auto& t : th) t.join();
     }
-    g->gathered = false;
     if (gpu_ms) *gpu_ms = *std::max_element(ms.begin(), ms.end());
     return gctx_rc(g, rc);
 }
@@ -2988,7 +3000,8 @@ PT_API int pt_group_gather(pt_group* g, float* host_ms)
         PT_GHIP_CHECK(g, hipSetDevice(g->ctx[i]->device));
         PT_GHIP_CHECK(g, hipStreamSynchronize(g->ctx[i]->stream));
     }
-    g->gathered = true;
+    g->gatherEpoch.clear();
+    for (pt_context* c : g->ctx) g->gatherEpoch.push_back(c->epoch);
     if (host_ms) *host_ms = std::chrono::duration<float, std::milli>(std::chrono::steady_clock::now() - t0).count();
     return PT_OK;
 }
@@ -2996,7 +3009,7 @@ PT_API int pt_group_gather(pt_group* g, float* host_ms)
 PT_API int pt_group_read_accum(pt_group* g, float* dst)
 {
     if (!g || !dst) return PT_ERR_ARG;
-    if (!g->gathered) {
+    if (!group_gathered(g)) {
         const int rc = pt_group_gather(g, nullptr);
         if (rc != PT_OK) return rc;
     }
@@ -3008,7 +3021,7 @@ PT_API int pt_group_read_accum(pt_group* g, float* dst)
 PT_API int pt_group_tonemap(pt_group* g, uint32_t frames, uint8_t* dst)
 {
     if (!g || !dst) return PT_ERR_ARG;
-    if (!g->gathered) {
+    if (!group_gathered(g)) {
         const int rc = pt_group_gather(g, nullptr);
         if (rc != PT_OK) return rc;
     }

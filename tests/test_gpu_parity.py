@@ -304,6 +304,59 @@ def test_group_rccl_gather_single_device(gpu_available, scenes):
     assert_bitexact(g.get_hdr_image_data(), ref.hdr(), "group getHDRImageData")
 
 
+def test_group_python_api_routes_through_the_group(gpu_available, scenes):
+    # a device group's Python methods act on the whole group -- knobs on every context,
+    # render_raw through pt_group_render, tonemap / rng_state over the full image -- and the
+    # per-context diagnostics refuse instead of returning one device's share
+    W, H = 72, 53
+    scene = scenes / "test_shapes.scene.json"
+    g = pa.Pathtracer(W, H, devices=[0])
+    assert g.band_rows == 8                      # the C++ constructor's and the CLI's default
+    cam = g.load_scene(str(scene))
+    single = pa.Pathtracer(W, H)
+    single.load_scene(str(scene))
+    assert np.array_equal(g.rng_state(), single.rng_state())
+    g.set_kernel_variant(20)
+    g.set_schedule(1)
+    g.set_sample_groups(1)
+    ms = g.render_raw(cam, 4, 2, True)
+    assert ms > 0.0
+    single.render_raw(cam, 4, 2, True)
+    assert np.array_equal(bits(g.accum()), bits(single.accum()))
+    assert np.array_equal(g.rng_state(), single.rng_state())
+    assert np.array_equal(g.tonemap(8), single.tonemap(8))
+    # a direct launch after a gather must not leave the gathered image stale
+    g.gather()
+    g.render_raw(cam, 4, 1, False)
+    single.render_raw(cam, 4, 1, False)
+    assert np.array_equal(bits(g.accum()), bits(single.accum()))
+    st = single.rng_state()
+    st[3, 5, 0] ^= 1
+    g.set_rng_state(st)
+    assert np.array_equal(g.rng_state(), st)
+    for call in (g.tile_costs, g.group_stats, lambda: g.render_instrumented(cam, 1, 1, True)):
+        with pytest.raises(pa.PathtracerError):
+            call()
+
+
+def test_group_two_devices(gpu_available, scenes):
+    # the multi-device group (RCCL send/recv across devices, one host thread per device)
+    # against the single-context render, bit for bit; needs two visible GPUs
+    if pa.device_count() < 2:
+        pytest.skip("one GPU visible")
+    W, H = 200, 120
+    scene = scenes / "generated_scene.scene.json"
+    g = pa.Pathtracer(W, H, devices=[0, 1])
+    cam = g.load_scene(str(scene))
+    single = pa.Pathtracer(W, H)
+    single.load_scene(str(scene))
+    g.render(cam, 8, True, chunks=3)
+    single.render(cam, 8, True, chunks=3)
+    assert np.array_equal(bits(g.accum()), bits(single.accum()))
+    assert np.array_equal(g.rng_state(), single.rng_state())
+    assert np.array_equal(g.get_image_data(), single.get_image_data())
+
+
 def test_c2_exact_size(gpu_available, scenes):
     # BASELINE config C2 exactly: cornell_box 512x512, 64 spp as the headless loop runs it (8
     # render() calls of 8), bit-exact against the oracle; a cold launch (cost pre-pass first)
@@ -366,6 +419,24 @@ def test_full_resolution_row_subset(gpu_available, scenes):
     pt.render(cam, 8, True, chunks=1)
     ref.render(osc.camera, 8, True, chunks=1)
     assert_bitexact(pt.accum(), ref.accum, "1080p row subset")
+
+
+def test_full_frame_bitexact_and_nan_pixels(gpu_available, scenes):
+    # BASELINE config C3 geometry, the whole 1920x1080 frame at 32 spp (4 render() calls of 8)
+    # against the oracle: every word, and the pixels poisoned by the reference's 0/0 VNDF pdf
+    # (MonteCarlo.h:110-113; LAMBERT_GGX with VdotH clamped to 0) counted on both sides -- the one
+    # full-frame statistic a change in the pdf path would move
+    W, H = 1920, 1080
+    pt, cam, ref, osc = pair(scenes / "generated_scene.scene.json", W, H)
+    pt.render(cam, 8, True, chunks=4)
+    ref.render(osc.camera, 8, True, chunks=4)
+    acc = pt.accum()
+    nan_gpu = int((~np.isfinite(acc)).any(-1).sum())
+    nan_ref = int((~np.isfinite(ref.accum)).any(-1).sum())
+    print(f"NaN pixels at 1080p x 32 spp: gpu {nan_gpu}, oracle {nan_ref}")
+    assert nan_gpu == nan_ref
+    assert_bitexact(acc, ref.accum, "1080p full frame x 32 spp")
+    assert np.array_equal(pt.rng_state(), ref.rng_array())
 
 
 def test_full_size_determinism(gpu_available, scenes):

@@ -79,3 +79,21 @@ def test_groups_equal_plain_launch_patch_and_resume(gpu_available, scenes, round
     assert st["dead_ends"][0] > 0, st                    # guesses missed somewhere: the later passes ran
     if rounds:
         assert st["patch_rounds"] >= 1, st
+
+
+def test_groups_refused_beyond_the_fold_word(gpu_available, scenes):
+    # the fold state packs (sample in call, call) as sIdx | c << 16, so a launch of more
+    # than 65,535 render() calls (or spp) must not run grouped; forced groups then run plain and the
+    # result equals the launch without groups, bit for bit
+    W, H, chunks = 16, 16, 70000
+    a = pa.Pathtracer(W, H)
+    cam = a.load_scene(str(scenes / "cornell_box.scene.json"))
+    b = pa.Pathtracer(W, H)
+    b.load_scene(str(scenes / "cornell_box.scene.json"))
+    a.set_sample_groups(2)
+    b.set_sample_groups(1)
+    a.render(cam, 1, True, chunks=chunks)
+    assert a.last_sample_groups == 0
+    b.render(cam, 1, True, chunks=chunks)
+    assert np.array_equal(a.accum().view(np.uint32), b.accum().view(np.uint32))
+    assert np.array_equal(a.rng_state(), b.rng_state())

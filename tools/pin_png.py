@@ -19,11 +19,17 @@ sys.path.insert(0, str(ROOT))
 import pathtracercuda_amd as pa  # noqa: E402
 
 ap = argparse.ArgumentParser()
-ap.add_argument("--scene", default="cornell_box")
+ap.add_argument("--scene", default="cornell_box", choices=["cornell_box"])
 ap.add_argument("--spp", type=int, default=4096)
 ap.add_argument("--per-call", type=int, default=1, help="spp per render() call (1 = the windowed loop)")
 ap.add_argument("--out", default="gpurun_out/pin")
+ap.add_argument("--corr", action="store_true", help="print the path-level pin of tests/pin.py as JSON and exit")
 a = ap.parse_args()
+if a.corr:
+    sys.path.insert(0, str(ROOT / "tests"))
+    import pin  # noqa: E402
+    print(json.dumps(pin.reference_pin(ROOT, ROOT / "scenes")))
+    sys.exit(0)
 ref = np.load(ROOT / "tests" / "golden" / f"{a.scene}_4096spp_ref8.npz")["rgb"].astype(np.int16)
 H, W, _ = ref.shape
 pt = pa.Pathtracer(W, H)
