@@ -200,7 +200,6 @@ class Run:
     camera, the gather buffers of the torchrun path."""
 
     def __init__(self, cfg, W, H, spp, rank, n, local_rank, band_rows, mode):
-        import torch
         import pathtracercuda_amd as pa
         from pathtracercuda_amd.distributed import global_rows, max_rows
 
@@ -220,6 +219,7 @@ class Run:
                                     row_stride=n if self.dist_on else 1, band_rows=self.band_rows)
         self.cam = self.pt.load_scene(scene_path(cfg["scene"]))
         if self.dist_on:
+            import torch
             dev = f"cuda:{local_rank}"
             self.send = torch.zeros((max_rows(H, n, self.band_rows), W, 4), dtype=torch.float32, device=dev)
             self.recv = [torch.zeros_like(self.send) for _ in range(n)] if rank == 0 else None
@@ -265,16 +265,19 @@ class Run:
 
 
 def timed(run, steps, warmup, local_rank, dist_on):
-    import torch
-    import torch.distributed as dist
+    if run.mode == "group":
+        # pt_group_render and pt_group_gather return after every device's stream is idle (and this
+        # process does not load torch: see main), so the group's calls are their own barrier
+        def barrier_sync():
+            pass
+    else:
+        import torch
+        import torch.distributed as dist
 
-    devices = range(run.n) if run.mode == "group" else [local_rank]
-
-    def barrier_sync():
-        for d in devices:
-            torch.cuda.synchronize(d)
-        if dist_on:
-            dist.barrier()
+        def barrier_sync():
+            torch.cuda.synchronize(local_rank)
+            if dist_on:
+                dist.barrier()
 
     for _ in range(warmup):
         run.step()
@@ -287,6 +290,8 @@ def timed(run, steps, warmup, local_rank, dist_on):
     barrier_sync()
     elapsed = time.perf_counter() - t0
     if dist_on:
+        import torch
+        import torch.distributed as dist
         t = torch.tensor([elapsed, kernel_ms], dtype=torch.float64, device=f"cuda:{local_rank}")
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed, kernel_ms = float(t[0]), float(t[1])
@@ -367,13 +372,13 @@ def main():
         W = int(round(W * math.sqrt(n) / 8.0)) * 8
         H = int(round(H * math.sqrt(n) / 8.0)) * 8
 
-    if mode == "group":
-        # the device group's communicators are created before torch touches any GPU
-        first = Run(cfg, W, H, spp, 0, n, 0, args.band_rows, mode)
-    import torch
-    import torch.distributed as dist
-
     dist_on = mode == "torchrun"
+    if mode != "group":
+        # torch brings its own copy of the HIP runtime (torch/lib/libamdhip64.so): it must be loaded
+        # before libpt_hip.so binds one, so that the process has a single runtime.  The device-group
+        # path needs no torch at all (its calls synchronise every device themselves) and loads none.
+        import torch
+        import torch.distributed as dist
     if dist_on:
         torch.cuda.set_device(local_rank)
         dist.init_process_group("nccl", device_id=torch.device("cuda", local_rank))
@@ -387,7 +392,7 @@ def main():
         dist.all_reduce(t)
         return dict(zip(keys, [float(x) for x in t]))
 
-    run = first if mode == "group" else Run(cfg, W, H, spp, rank, n, local_rank, args.band_rows, mode)
+    run = Run(cfg, W, H, spp, rank, n, local_rank, args.band_rows, mode)
     st = stats_all(run.instrument())
     elapsed, kernel_ms = timed(run, args.steps, args.warmup, local_rank, dist_on)
     main_rec = record(cfg, run, elapsed, kernel_ms, args.steps, st, n)

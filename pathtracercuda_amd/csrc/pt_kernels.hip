@@ -48,7 +48,8 @@ __device__ __forceinline__ float* lds_f() { return reinterpret_cast<float*>(lds4
 struct DevTex {
     const float4* texels;
     uint32_t width, height;
-    uint32_t pad0, pad1;
+    float fwidth, fheight;      // (float)width, (float)height, converted once on the host: a uniform
+                                // conversion in the kernel would be a VALU result held in a VGPR
 };
 
 struct DevCamera {
@@ -67,6 +68,7 @@ struct TraceParams {
     DevTex skyTex;              // the skybox's descriptor itself (kernel argument: scalar loads, no
                                 // dependent fetch from the texture table per miss)
     uint32_t width, height, rowOffset, rowStride, rows;
+    float fwidth, fheight;      // (float)width, (float)height (host-converted, see DevTex)
     uint32_t bandShift;         // rows are tiled in bands of 1 << bandShift rows (global_row)
     uint32_t spp, chunks, ignoreFirst;
     uint32_t tilesX, tilesY;
@@ -74,7 +76,8 @@ struct TraceParams {
     const float4* cnodes;       // child-box records (4 per interior node), see traverse_cb
     uint32_t cnodeCount, rootWord;
     float rootBox[6];           // (min.x, max.x, min.y, max.y, min.z, max.z) of the root
-    const uint32_t* order;      // tile dispatch order (null: row-major), see "Tile scheduling"
+    const uint32_t* order;      // tile dispatch order as packed tile coordinates (tileY << 16 | tileX),
+                                // see "Tile scheduling"; null only with scatterWaves
     uint32_t scatterWaves;      // != 0: scattered pixel mapping over this many waves (pixel_of)
     uint32_t* tileCursor;       // persistent variants: {next dispatch slot, waves finished}, rewound by the last wave
     uint32_t numSlots;          // dispatch slots = 8x8 tiles
@@ -133,7 +136,7 @@ __host__ __device__ inline uint32_t global_row(uint32_t ly, uint32_t offset, uin
 // ---------------------------------------------------------------------------------------------
 PT_DEV f3 tex2d(const DevTex& t, float u, float v)
 {
-    const float W = (float)t.width, H = (float)t.height;
+    const float W = t.fwidth, H = t.fheight;
     const float uw = u - floorf(u);
     const float x = uw * W - 0.5f;
     const float y = v * H - 0.5f;
@@ -869,8 +872,8 @@ struct PathState {
 // camera ray of one sample (trace.cu:190-192, Camera.inl:25-28): two uniforms, x then y
 PT_DEV void camera_ray(const TraceParams& P, float fx, float fy, Xorwow& rng, f3& o, f3& d)
 {
-    const float u = (fx + uniform(rng)) / (float)P.width;
-    const float v = (fy + uniform(rng)) / (float)P.height;
+    const float u = (fx + uniform(rng)) / P.fwidth;
+    const float v = (fy + uniform(rng)) / P.fheight;
     o = P.cam.origin;
     d = normalize(add(add(P.cam.llc, scale(u, P.cam.horizontal)), scale(v, P.cam.vertical)));
 }
@@ -1231,7 +1234,7 @@ PT_DEV PixelCtx pixel_of(const TraceParams& P, uint32_t tile, uint32_t lane)
         pc.py = global_row(ly, P.rowOffset, P.rowStride, P.bandShift);
         return pc;
     }
-    const uint32_t tileX = tile % P.tilesX, tileY = tile / P.tilesX;
+    const uint32_t tileX = tile & 0xffffu, tileY = tile >> 16;   // packed (order entries)
     pc.px = tileX * 8u + (lane & 7u);
     const uint32_t ly = tileY * 8u + (lane >> 3);
     pc.valid = tileY < P.tilesY && pc.px < P.width && ly < P.rows;
@@ -1276,14 +1279,19 @@ PT_DEV void load_pixel(const TraceParams& P, const PixelCtx& pc, Xorwow& rng, Pa
 
 PT_DEV void store_pixel(const TraceParams& P, const PixelCtx& pc, const Xorwow& rng, const PathState& ps)
 {
-    P.rng[pc.li] = rng.d;
-    P.rng[pc.npix + pc.li] = rng.v0;
-    P.rng[2 * pc.npix + pc.li] = rng.v1;
-    P.rng[3 * pc.npix + pc.li] = rng.v2;
-    P.rng[4 * pc.npix + pc.li] = rng.v3;
-    P.rng[5 * pc.npix + pc.li] = rng.v4;
+    // The pixel index passes through an empty asm so the store addresses are recomputed here from
+    // one 32-bit register: otherwise the compiler reuses the seven 64-bit addresses of load_pixel and
+    // keeps them live (spilled) across the whole tile.  Contexts hold < 2^30 pixels (pt_create).
+    uint32_t li = (uint32_t)pc.li;
+    asm volatile("" : "+v"(li));
+    P.rng[li] = rng.d;
+    P.rng[pc.npix + li] = rng.v0;
+    P.rng[2 * pc.npix + li] = rng.v1;
+    P.rng[3 * pc.npix + li] = rng.v2;
+    P.rng[4 * pc.npix + li] = rng.v3;
+    P.rng[5 * pc.npix + li] = rng.v4;
     const float* a = lds_f() + ps.acc;
-    P.accum[pc.li] = make_float4(a[0], a[64], a[128], 1.0f);   // trace.cu:198, once per launch
+    P.accum[li] = make_float4(a[0], a[64], a[128], 1.0f);   // trace.cu:198, once per launch
 }
 
 // ---------------------------------------------------------------------------------------------
@@ -1332,7 +1340,7 @@ __global__ void __launch_bounds__(WPB * 64, MINW) trace_kernel(TraceParams P)
         pos = slot / J;
         grp = slot - pos * J;                        // item within the tile (ssg_load)
     }
-    tile = P.order ? P.order[pos] : pos;
+    tile = P.order ? P.order[pos] : pos;          // packed coordinates (scatter mode: wave index)
     const PixelCtx pc = pixel_of(P, tile, lane);
     const uint64_t tWave = __builtin_amdgcn_s_memtime();
     const bool run = pc.valid && (!AUX || !P.fold || (P.fold[F_FLAG * pc.npix + pc.li] & 1u));
@@ -1409,10 +1417,11 @@ __global__ void __launch_bounds__(WPB * 64, MINW) trace_kernel(TraceParams P)
             P.pairsOut[pc.npix + pc.li] = -1.0f;      // odd-length fraction unknown
         }
     }
-    if (P.tileCost && lane == 0 && tile < P.tilesX * P.tilesY) {
+    if (P.tileCost && lane == 0 && (tile >> 16) < P.tilesY) {
         const uint32_t cyc = (uint32_t)min(__builtin_amdgcn_s_memtime() - tWave, (uint64_t)0xffffffffu);
-        if (SSG) atomicAdd(&P.tileCost[tile], cyc / P.ssgG);   // zeroed before the launch (idle items add ~0)
-        else P.tileCost[tile] = cyc;
+        const uint32_t lin = (tile >> 16) * P.tilesX + (tile & 0xffffu);
+        if (SSG) atomicAdd(&P.tileCost[lin], cyc / P.ssgG);   // zeroed before the launch (idle items add ~0)
+        else P.tileCost[lin] = cyc;
     }
     if (!PERSIST) break;
     slot = wave_fetch(P.tileCursor, 1u);
@@ -1476,8 +1485,8 @@ PT_DEV bool ssg_pixel(const TraceParams& P, size_t gid, uint32_t& pos, uint32_t&
     pos = (uint32_t)(gid >> 6);                      // position in the order: the per-item buffers' index
     lane = (uint32_t)(gid & 63u);
     if (pos >= P.ssgTiles) return false;
-    const uint32_t tile = P.order ? P.order[pos] : pos;
-    const uint32_t tileX = tile % P.tilesX, tileY = tile / P.tilesX;
+    const uint32_t tile = P.order[pos];              // packed tile coordinates
+    const uint32_t tileX = tile & 0xffffu, tileY = tile >> 16;
     const uint32_t px = tileX * 8u + (lane & 7u), ly = tileY * 8u + (lane >> 3);
     li = (size_t)ly * P.width + px;
     return tileY < P.tilesY && px < P.width && ly < P.rows;
@@ -1823,6 +1832,7 @@ struct pt_context {
     // tile scheduling: per-tile cost of the last launch and the cost-sorted dispatch order
     uint32_t* tileCost = nullptr;
     uint32_t* order = nullptr;
+    uint32_t* rowMajor = nullptr;     // the row-major order (packed coordinates), before costs are known
     uint32_t* tileCursor = nullptr;   // persistent variants
     uint32_t* sortKeys = nullptr; // radix-sort scratch: sorted costs, tile ids, temp storage
     uint32_t* tileIds = nullptr;
@@ -2052,6 +2062,11 @@ PT_API int pt_create_banded(int device, uint32_t width, uint32_t height, uint32_
     if (!out || width == 0 || height == 0 || band_stride == 0) return PT_ERR_ARG;
     *out = nullptr;
     if (band_rows == 0 || band_rows > 256 || (band_rows & (band_rows - 1)) != 0) return PT_ERR_ARG;
+    // tiles are addressed by packed 16-bit coordinates (tileY << 16 | tileX), pixels by 32-bit indices
+    {
+        const uint64_t r = pt_band_rows(height, band_rows, band_offset, band_stride);
+        if (width > 8u * 0xffffu || r > 8u * 0xfffeu || r * width >= (1ull << 30)) return PT_ERR_ARG;
+    }
     const uint32_t row_offset = band_offset, row_stride = band_stride;
     int n = 0;
     if (hipGetDeviceCount(&n) != hipSuccess || n == 0) return PT_ERR_NO_DEVICE;
@@ -2101,6 +2116,7 @@ PT_API void pt_destroy(pt_context* ctx)
     (void)hipFree(ctx->cnodes);
     (void)hipFree(ctx->tileCost);
     (void)hipFree(ctx->order);
+    (void)hipFree(ctx->rowMajor);
     (void)hipFree(ctx->tileCursor);
     (void)hipFree(ctx->ldr);
     (void)hipFree(ctx->sortKeys);
@@ -2265,6 +2281,8 @@ PT_API int pt_set_texture(pt_context* ctx, uint32_t handle, const float* rgba, u
     t.texels = mem;
     t.width = width;
     t.height = height;
+    t.fwidth = (float)width;
+    t.fheight = (float)height;
     ctx->orderStale = true;
     PT_HIP_CHECK(ctx, hipMemcpy(ctx->texTable, ctx->hostTex, sizeof(ctx->hostTex), hipMemcpyHostToDevice));
     return PT_OK;
@@ -2477,6 +2495,8 @@ static int render_impl(pt_context* ctx, const pt_camera* cam, uint32_t spp, uint
     if (ctx->skybox != 0) P.skyTex = ctx->hostTex[ctx->skybox - 1];
     P.width = ctx->width;
     P.height = ctx->height;
+    P.fwidth = (float)ctx->width;
+    P.fheight = (float)ctx->height;
     P.rowOffset = ctx->rowOffset;
     P.rowStride = ctx->rowStride;
     P.rows = ctx->rows;
@@ -2529,8 +2549,15 @@ static int render_impl(pt_context* ctx, const pt_camera* cam, uint32_t spp, uint
                                                          ctx->tileIds, ctx->order, tiles, 0, 32, ctx->stream));
         PT_HIP_CHECK(ctx, hipMalloc(&ctx->sortTemp, ctx->sortTempBytes ? ctx->sortTempBytes : 4));
         PT_HIP_CHECK(ctx, hipMemsetAsync(ctx->tileCost, 0, (size_t)tiles * sizeof(uint32_t), ctx->stream));
-        std::vector<uint32_t> ident((size_t)tiles + 64);              // slots past the last tile stay invalid
-        for (size_t i = 0; i < ident.size(); ++i) ident[i] = (uint32_t)i;
+        // tiles as packed coordinates (tileY << 16 | tileX: the kernel needs no division by tilesX);
+        // slots past the last tile stay invalid (tileY = tilesY)
+        std::vector<uint32_t> ident((size_t)tiles + 64);
+        for (size_t i = 0; i < ident.size(); ++i)
+            ident[i] = i < tiles ? ((uint32_t)(i / P.tilesX) << 16) | (uint32_t)(i % P.tilesX) : P.tilesY << 16;
+        (void)hipFree(ctx->rowMajor);
+        ctx->rowMajor = nullptr;
+        PT_HIP_CHECK(ctx, hipMalloc(&ctx->rowMajor, ident.size() * sizeof(uint32_t)));
+        PT_HIP_CHECK(ctx, hipMemcpy(ctx->rowMajor, ident.data(), ident.size() * sizeof(uint32_t), hipMemcpyHostToDevice));
         PT_HIP_CHECK(ctx, hipMemcpy(ctx->order, ident.data(), ident.size() * sizeof(uint32_t), hipMemcpyHostToDevice));
         PT_HIP_CHECK(ctx, hipMemcpy(ctx->tileIds, ident.data(), (size_t)tiles * sizeof(uint32_t), hipMemcpyHostToDevice));
         ctx->orderTiles = tiles;
@@ -2541,9 +2568,10 @@ static int render_impl(pt_context* ctx, const pt_camera* cam, uint32_t spp, uint
         ctx->lastCam = *cam;
     }
     const bool sorted = ctx->schedule == 0;
-    P.order = (sorted && ctx->orderValid) ? ctx->order : nullptr;
+    P.order = (sorted && ctx->orderValid) ? ctx->order : ctx->rowMajor;
     P.tileCost = sorted ? ctx->tileCost : nullptr;
     P.scatterWaves = ctx->schedule == 2 ? (uint32_t)(((size_t)ctx->rows * ctx->width + 63) / 64) : 0u;
+    if (P.scatterWaves) P.order = nullptr;          // scattered mapping: slot = wave index
     if (!ctx->tileCursor) {
         PT_HIP_CHECK(ctx, hipMalloc(&ctx->tileCursor, 2 * sizeof(uint32_t)));
         PT_HIP_CHECK(ctx, hipMemset(ctx->tileCursor, 0, 2 * sizeof(uint32_t)));
@@ -2583,7 +2611,7 @@ static int render_impl(pt_context* ctx, const pt_camera* cam, uint32_t spp, uint
         Q.chunks = 1;
         Q.ignoreFirst = 1;
         Q.discard = 1;
-        Q.order = nullptr;
+        Q.order = ctx->rowMajor;
         Q.pairsOut = guesses && ssg_reserve(ctx, tiles, 0, 0, 0) ? ctx->pairs : nullptr;
         if (Q.pairsOut) ctx->pairsValid = true;
         PT_HIP_CHECK(ctx, Q.pairsOut ? launch_grouped<2>(variant, Q, ctx->stream) : launch_variant<false>(variant, Q, ctx->stream));
