@@ -131,6 +131,16 @@ def algorithmic_bytes(stats: dict) -> float:
             + SKY_B * stats["sky_lookups"])
 
 
+def kernel_source_sha() -> str:
+    """sha256 (16 hex) of the kernel sources the trace kernel is built from: a committed PMC profile
+    records the same digest, so a profile of another kernel cannot pair with this build unnoticed."""
+    import hashlib
+    h = hashlib.sha256()
+    for f in ("pathtracercuda_amd/csrc/pt_kernels.hip", "pathtracercuda_amd/csrc/pt_math.h"):
+        h.update((ROOT / f).read_bytes())
+    return h.hexdigest()[:16]
+
+
 def load_profile(workload: str):
     """Per-launch counters of the trace kernel from the newest committed rocprofv3 --pmc summary of
     this workload (profiles/*pmc_traffic*.json): HBM bytes (FETCH_SIZE x2 + WRITE_SIZE, gfx950
@@ -212,8 +222,16 @@ class Run:
         self.gather_ms = 0.0
         if mode == "group":
             # the product's multi-device Pathtracer: one context per GPU, RCCL communicators from
-            # ncclCommInitAll, created before any other GPU work of this process
-            self.pt = pa.Pathtracer(W, H, devices=list(range(n)), band_rows=self.band_rows)
+            # ncclCommInitAll.  RCCL prints its version banner on stdout; it goes to stderr here so
+            # that stdout carries only the JSON line
+            sys.stdout.flush()
+            saved = os.dup(1)
+            os.dup2(2, 1)
+            try:
+                self.pt = pa.Pathtracer(W, H, devices=list(range(n)), band_rows=self.band_rows)
+            finally:
+                os.dup2(saved, 1)
+                os.close(saved)
         else:
             self.pt = pa.Pathtracer(W, H, device=local_rank, row_offset=rank if self.dist_on else 0,
                                     row_stride=n if self.dist_on else 1, band_rows=self.band_rows)
@@ -299,7 +317,7 @@ def timed(run, steps, warmup, local_rank, dist_on):
 
 
 LANE_KEYS = ("node_tests", "prim_tests", "hits", "sky_lookups", "segments", "wave_node_iters", "wave_prim_iters",
-             "wave_hits", "wave_sky")
+             "wave_hits", "wave_sky", "leaf_rounds", "family_execs", "family_execs_compacted")
 
 
 def lane_utilisation(st):
@@ -311,8 +329,15 @@ def lane_utilisation(st):
     if "d_hits" in st:                     # the default kernel's instrumented chunk (Run.instrument)
         st = {k: st["d_" + k] for k in LANE_KEYS}
     visits = (st["node_tests"] + st["segments"]) / 2.0
-    return {"interior_walk": ratio(visits, st["wave_node_iters"]), "leaf_tests": ratio(st["prim_tests"], st["wave_prim_iters"]),
-            "hit_shading": ratio(st["hits"], st["wave_hits"]), "sky_shading": ratio(st["sky_lookups"], st["wave_sky"])}
+    out = {"interior_walk": ratio(visits, st["wave_node_iters"]), "leaf_tests": ratio(st["prim_tests"], st["wave_prim_iters"]),
+           "hit_shading": ratio(st["hits"], st["wave_hits"]), "sky_shading": ratio(st["sky_lookups"], st["wave_sky"])}
+    if st.get("family_execs"):
+        # leaf tests per shape-family path (plane / cube / quadric): lane utilisation of the family
+        # paths as run, and the executions a perfect cross-lane compaction by family would need
+        out["leaf_family_paths"] = ratio(st["prim_tests"], st["family_execs"])
+        out["leaf_family_execs_per_round"] = round(st["family_execs"] / max(st["leaf_rounds"], 1), 3)
+        out["leaf_family_execs_per_round_compacted"] = round(st["family_execs_compacted"] / max(st["leaf_rounds"], 1), 3)
+    return out
 
 
 def record(cfg, run, elapsed, kernel_ms, steps, st, n, with_profile=True):
@@ -349,6 +374,9 @@ def record(cfg, run, elapsed, kernel_ms, steps, st, n, with_profile=True):
             "hbm_GBs_measured": round(prof["bytes_per_launch"] * scale / avg_launch_s / 1e9, 1),
             "hbm_frac_measured": round(prof["bytes_per_launch"] * scale / avg_launch_s / 1e9 / HBM_PEAK_GBS, 5),
             "profile": src + ("" if scale == 1.0 else f" (per-launch counts x {scale:.4f}: this GPU's share)"),
+            "profile_commit": prof.get("commit"),
+            "profile_kernel_sha": prof.get("kernel_sha"),
+            "profile_matches_build": prof.get("kernel_sha") == kernel_source_sha(),
         })
     return {"value": round(total_samples / elapsed / 1e6, 3), "unit": "Msamples/s", "ms_per_step": round(elapsed * 1e3 / steps, 3),
             "workload": workload, "roofline": roof}

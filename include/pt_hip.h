@@ -94,6 +94,13 @@ typedef struct pt_render_stats {
     uint64_t cycles_shading;
     uint64_t cycles_total;
     uint64_t cycles_lane_idle;  /* resumable variants: lane cycles spent done while the tile still ran */
+    /* leaf tests by shape family (plane = disk/quad, cube, quadric: the three code paths of the
+     * primitive test), resumable variants: leaf rounds (the wave's pending leaves after an interior
+     * walk), family-path executions as run (per leaf position, one per family present), and as a
+     * perfect cross-lane compaction would run them (per leaf round, ceil(pairs of the family / 64)) */
+    uint64_t leaf_rounds;
+    uint64_t family_execs;
+    uint64_t family_execs_compacted;
 } pt_render_stats;
 
 typedef struct pt_context pt_context;
@@ -187,6 +194,11 @@ PT_API int pt_set_kernel_variant(pt_context *ctx, int variant);
  * rebuilt on the device from the latest launch), 1 = always row-major.  Results are identical;
  * only the launch tail changes. */
 PT_API int pt_set_schedule(pt_context *ctx, int mode);
+
+/* Tuning knob for measurements: persistent trace-kernel grids hold at most workgroups_per_cu
+ * workgroups (of four waves, one per SIMD) per CU, i.e. that many waves per SIMD (0 = as many as
+ * fit, the default).  Results are identical. */
+PT_API int pt_set_occupancy(pt_context *ctx, uint32_t workgroups_per_cu);
 
 /* Speculative sample groups.  A pixel's samples are one serial XORWOW stream
  * (trace.cu:183-193), so a launch with fewer 8x8 tiles than about four per wave slot of the chip

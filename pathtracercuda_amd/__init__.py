@@ -299,6 +299,12 @@ class Pathtracer:
         for c in self._contexts():
             N.check_ctx(N.hip().pt_set_kernel_variant(c, int(variant)), c)
 
+    def set_occupancy(self, workgroups_per_cu: int) -> None:
+        """Persistent grids hold at most this many 4-wave workgroups per CU (waves per SIMD); 0 = all
+        that fit (pt_set_occupancy).  A measurement knob: results are identical."""
+        for c in self._contexts():
+            N.check_ctx(N.hip().pt_set_occupancy(c, int(workgroups_per_cu)), c)
+
     def set_schedule(self, mode: int) -> None:
         """0 = cost-sorted tile dispatch (default), 1 = row-major (pt_set_schedule), every device."""
         for c in self._contexts():

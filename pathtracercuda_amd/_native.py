@@ -43,7 +43,8 @@ class PtRenderStats(C.Structure):
                 ("wave_node_iters", C.c_uint64), ("wave_prim_iters", C.c_uint64), ("wave_hits", C.c_uint64),
                 ("wave_sky", C.c_uint64), ("wave_segments", C.c_uint64), ("cycles_node_walk", C.c_uint64),
                 ("cycles_leaf_tests", C.c_uint64), ("cycles_shading", C.c_uint64), ("cycles_total", C.c_uint64),
-                ("cycles_lane_idle", C.c_uint64)]
+                ("cycles_lane_idle", C.c_uint64), ("leaf_rounds", C.c_uint64), ("family_execs", C.c_uint64),
+                ("family_execs_compacted", C.c_uint64)]
 
 
 # symbol -> (restype, argtypes); the CPU test suite checks that every declaration in include/*.h
@@ -70,6 +71,7 @@ _HIP_SYMBOLS = {
     "pt_local_rows": (C.c_uint32, [C.c_void_p]),
     "pt_read_tile_costs": (C.c_int, [C.c_void_p, P(C.c_uint32), C.c_uint32]),
     "pt_set_kernel_variant": (C.c_int, [C.c_void_p, C.c_int]),
+    "pt_set_occupancy": (C.c_int, [C.c_void_p, C.c_uint32]),
     "pt_set_schedule": (C.c_int, [C.c_void_p, C.c_int]),
     "pt_set_sample_groups": (C.c_int, [C.c_void_p, C.c_int]),
     "pt_last_sample_groups": (C.c_int, [C.c_void_p]),

@@ -103,6 +103,7 @@ struct TraceParams {
     uint32_t* ssgCount;         // [item][64] samples logged
     uint32_t* fold;             // [kFoldWords][rows*width] fold state (ssg_fold_kernel); AUX resume input
     DevCamera cam;
+    uint32_t occCap;            // host only: persistent grids hold at most this many workgroups per CU (0 = all)
 };
 
 // Speculative sample groups: window of a group's start offset in which an earlier group's parse can
@@ -116,6 +117,7 @@ static inline uint32_t ssg_window_words(uint32_t G, uint32_t n)
     return G == 2 ? (n * 6u + 256u + 63u) / 64u : kWinWords;
 }
 constexpr uint32_t kFoldBatch = 16;       // samples the fold loads at once
+constexpr uint32_t kStatWords = 19;       // counters of an instrumented launch (pt_render_stats)
 constexpr uint32_t kStartWords = 8;       // start record: offset, d, v0..v4, stop offset (last group)
 enum : uint32_t { F_ACC = 0, F_COL = 3, F_SC = 6, F_DONE = 7, F_OFF = 8, F_H = 9, F_ST = 10, F_FLAG = 16, F_ODD = 17,
                   F_SQ = 18, kFoldWords = 19 };
@@ -285,7 +287,38 @@ struct Counters {
     // wave-level shader-clock cycles per phase (instrumented variant only)
     uint64_t cyc_node, cyc_leaf, cyc_shade, cyc_total;
     uint64_t cyc_lane_idle;     // per lane: cycles between finishing its pixel and the tile's end
+    uint32_t w_leaf_rounds, w_fam_exec, w_fam_ideal;   // leaf tests by shape family (pt_render_stats)
 };
+
+// Shape family of a primitive test's code path in prim_hit: 0 plane (disk, quad), 1 cube, 2 quadric.
+PT_DEV uint32_t shape_family(uint32_t type) { return (type == DISK || type == QUAD) ? 0u : (type == CUBE ? 1u : 2u); }
+
+// Instrumented variants: one leaf round -- the family-path executions a perfect cross-lane
+// compaction would need (ceil(pairs of the family / 64) per family) -- counted once per wave.
+PT_DEV void leaf_round_stats(const float4* __restrict__ prims, uint32_t off, uint32_t count, Counters& cnt)
+{
+    uint32_t nf[3] = {0u, 0u, 0u};
+    for (uint32_t k = 0; k < count; ++k) nf[shape_family(__float_as_uint(prims[4 * (off + k) + 3].x))]++;
+    uint32_t ideal = 0;
+#pragma unroll
+    for (int f = 0; f < 3; ++f) {
+        uint32_t total = 0;
+#pragma unroll
+        for (int b = 0; b < 8; ++b) total += (uint32_t)__popcll(__ballot((nf[f] >> b) & 1u)) << b;
+        ideal += (total + 63u) / 64u;
+    }
+    const unsigned long long m = __ballot(1);
+    if ((threadIdx.x & 63u) == (uint32_t)(__ffsll((long long)m) - 1)) { cnt.w_leaf_rounds++; cnt.w_fam_ideal += ideal; }
+}
+
+// One leaf position: the family paths the wave runs (one per family among its active lanes).
+PT_DEV void leaf_position_stats(const float4* __restrict__ prims, uint32_t p, Counters& cnt)
+{
+    const uint32_t f = shape_family(__float_as_uint(prims[4 * p + 3].x));
+    const uint32_t execs = (__ballot(f == 0u) != 0ull) + (__ballot(f == 1u) != 0ull) + (__ballot(f == 2u) != 0ull);
+    const unsigned long long m = __ballot(1);
+    if ((threadIdx.x & 63u) == (uint32_t)(__ffsll((long long)m) - 1)) cnt.w_fam_exec += execs;
+}
 
 // Adds the cycles since `t0` to `acc` once per wave and restarts the stamp.
 PT_DEV void wave_time(uint64_t& acc, uint64_t& t0)
@@ -634,8 +667,9 @@ PT_DEV uint32_t traverse_cb(const float4* __restrict__ cnodes, const float4* __r
         if (STATS) wave_time(cnt.cyc_node, tPhase);
         if (done) break;
         uint32_t leafOff = cur & 0xffffffu, leafCnt = cur >> 24;  // in-order leaf tests
+        if (STATS) leaf_round_stats(prims, leafOff, leafCnt, cnt);
         while (leafCnt > 0) {
-            if (STATS) { cnt.prim_tests++; wave_tick(cnt.w_prim); }
+            if (STATS) { cnt.prim_tests++; wave_tick(cnt.w_prim); leaf_position_stats(prims, leafOff, cnt); }
             float t;
             if (prim_hit(prims, leafOff, o, d, tMin, tMax, t)) {
                 tMax = t;
@@ -714,8 +748,9 @@ PT_DEV bool traverse_cb_phase(const float4* __restrict__ cnodes, const float4* _
         if (STATS) wave_time(cnt.cyc_node, tPhase);
         if (done) break;
         uint32_t leafOff = cur & 0xffffffu, leafCnt = cur >> 24;
+        if (STATS) leaf_round_stats(prims, leafOff, leafCnt, cnt);
         while (leafCnt > 0) {
-            if (STATS) { cnt.prim_tests++; wave_tick(cnt.w_prim); }
+            if (STATS) { cnt.prim_tests++; wave_tick(cnt.w_prim); leaf_position_stats(prims, leafOff, cnt); }
             float t;
             if (prim_hit(prims, leafOff, o, d, tMin, tMax, t)) {
                 tMax = t;
@@ -1041,6 +1076,9 @@ PT_DEV void flush_counters(const TraceParams& P, const Counters& cnt)
     atomicAdd(&P.stats[13], (unsigned long long)cnt.cyc_shade);
     atomicAdd(&P.stats[14], (unsigned long long)cnt.cyc_total);
     atomicAdd(&P.stats[15], (unsigned long long)cnt.cyc_lane_idle);
+    atomicAdd(&P.stats[16], (unsigned long long)cnt.w_leaf_rounds);
+    atomicAdd(&P.stats[17], (unsigned long long)cnt.w_fam_exec);
+    atomicAdd(&P.stats[18], (unsigned long long)cnt.w_fam_ideal);
 }
 
 // One atomic per wave: the first active lane adds n to *cursor and broadcasts the old value.
@@ -1843,6 +1881,7 @@ struct pt_context {
     bool orderValid = false;      // `order` holds a cost-sorted permutation
     bool orderStale = true;       // rebuild it after the next launch (scene, texture or camera changed)
     int schedule = 0;             // 0 = cost-sorted tiles (default), 1 = row-major
+    uint32_t occupancy = 0;       // tuning knob: workgroups per CU of persistent grids (0 = all that fit)
     // speculative sample groups
     int ssgMode = 0;              // 0 = automatic, 1 = off, G >= 2 = always G groups (tests)
     uint32_t patchRounds = 6;     // patch rounds before the remaining dead ends run plain
@@ -1937,6 +1976,13 @@ static hipError_t launch_one(const TraceParams& P, hipStream_t stream)
             cap = std::max(cus, 1) * std::max(perCu, 1);
             resident[dev & 63].store(cap);
         }
+        if (P.occCap) {                                // tuning knob (pt_set_occupancy): fewer waves per SIMD
+            int cus = 0;
+            if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) == hipSuccess && cus > 0)
+                cap = std::min(cap, cus * (int)P.occCap);
+            trace_kernel<STATS, SL, WPB, WW, MINW, PERSIST, MODE><<<(unsigned)cap, WPB * 64, lds, stream>>>(P);
+            return hipGetLastError();
+        }
         if (blocks <= (unsigned)cap) return launch_one<STATS, SL, WPB, WW, MINW, false, MODE>(P, stream);
         blocks = (unsigned)cap;
     }
@@ -1963,9 +2009,7 @@ static hipError_t launch_one(const TraceParams& P, hipStream_t stream)
 //       deferral, which costs a single pass of latency-bound waves 2.8 %
 //   48  small grids whose primitives fit in LDS too: records and primitives in LDS, 4 waves/SIMD,
 //       deferred hits
-#ifndef PT_V40_WW
-#define PT_V40_WW 13216     // variant 40's walk parameters (A/B builds override it: tools/build_snap.sh)
-#endif
+constexpr int kV40Walk = 13216;     // variant 40's walk parameters (SKYQ 1, DEFERQ 3, exit <= 16/64)
 template <bool STATS, int MODE = 0>
 static hipError_t launch_variant(int v, const TraceParams& P, hipStream_t stream)
 {
@@ -1975,7 +2019,7 @@ static hipError_t launch_variant(int v, const TraceParams& P, hipStream_t stream
     case 6: return launch_one<STATS, 1, 4, 1, 5, false, MODE>(P, stream);
     case 20: return launch_one<STATS, 0, 4, 3, 5, false, MODE>(P, stream);
     case 39: return launch_one<STATS, 1, 4, 224, 5, true, MODE>(P, stream);
-    case 40: return launch_one<STATS, 1, 4, PT_V40_WW, 5, true, MODE>(P, stream);
+    case 40: return launch_one<STATS, 1, 4, kV40Walk, 5, true, MODE>(P, stream);
     case 41: return launch_one<STATS, 0, 4, 13212, 5, true, MODE>(P, stream);
     case 46: return launch_one<STATS, 0, 4, 13212, 4, true, MODE>(P, stream);
     case 47: return launch_one<STATS, 1, 4, 224, 4, true, MODE>(P, stream);
@@ -1991,7 +2035,7 @@ static hipError_t launch_grouped(int v, const TraceParams& P, hipStream_t stream
 {
     switch (v) {
     case 39: return launch_one<false, 1, 4, 224, 5, true, MODE>(P, stream);
-    case 40: return launch_one<false, 1, 4, PT_V40_WW, 5, true, MODE>(P, stream);
+    case 40: return launch_one<false, 1, 4, kV40Walk, 5, true, MODE>(P, stream);
     case 41: return launch_one<false, 0, 4, 13212, 5, true, MODE>(P, stream);
     case 46: return launch_one<false, 0, 4, 13212, 4, true, MODE>(P, stream);
     default: return hipErrorInvalidValue;
@@ -2088,7 +2132,7 @@ PT_API int pt_create_banded(int device, uint32_t width, uint32_t height, uint32_
     if (hipMalloc(&ctx->accum, nalloc * sizeof(float4)) != hipSuccess) return bail(PT_ERR_HIP);
     if (hipMalloc(&ctx->rng, nalloc * 6 * sizeof(uint32_t)) != hipSuccess) return bail(PT_ERR_HIP);
     if (hipMalloc(&ctx->texTable, PT_MAX_TEXTURES * sizeof(DevTex)) != hipSuccess) return bail(PT_ERR_HIP);
-    if (hipMalloc(&ctx->stats, 16 * sizeof(unsigned long long)) != hipSuccess) return bail(PT_ERR_HIP);
+    if (hipMalloc(&ctx->stats, kStatWords * sizeof(unsigned long long)) != hipSuccess) return bail(PT_ERR_HIP);
     if (hipMemsetAsync(ctx->accum, 0, nalloc * sizeof(float4), ctx->stream) != hipSuccess) return bail(PT_ERR_HIP);
     if (hipMemcpyAsync(ctx->texTable, ctx->hostTex, sizeof(ctx->hostTex), hipMemcpyHostToDevice, ctx->stream) != hipSuccess)
         return bail(PT_ERR_HIP);
@@ -2395,6 +2439,25 @@ static bool ssg_reserve(pt_context* ctx, size_t tiles, size_t items, size_t samp
     return true;
 }
 
+// The sample-group logs of a context that launches plain again (up to ~15 GB at a 1080p rank share
+// at N = 8) are released; the per-pixel statistics (pairs, fold state) stay for the next guesses.
+static void ssg_release(pt_context* ctx)
+{
+    if (!ctx->ssgItems && !ctx->ssgSamples && !ctx->patchSamples && !ctx->ssgBitsWords) return;
+    (void)hipStreamSynchronize(ctx->stream);
+    for (void* q : {(void*)ctx->ssgStart, (void*)ctx->ssgCount, (void*)ctx->ssgBits, (void*)ctx->ssgLog,
+                    (void*)ctx->ssgEnd, (void*)ctx->patchLog, (void*)ctx->patchEnd})
+        (void)hipFree(q);
+    ctx->ssgStart = nullptr;
+    ctx->ssgCount = nullptr;
+    ctx->ssgBits = nullptr;
+    ctx->ssgLog = nullptr;
+    ctx->ssgEnd = nullptr;
+    ctx->patchLog = nullptr;
+    ctx->patchEnd = nullptr;
+    ctx->ssgItems = ctx->ssgSamples = ctx->patchSamples = ctx->ssgBitsWords = 0;
+}
+
 // Stable radix sort of (cost, tile) pairs, descending, into the dispatch order: deterministic, ties
 // in tile order.
 static int sort_order(pt_context* ctx, uint32_t tiles)
@@ -2578,7 +2641,8 @@ static int render_impl(pt_context* ctx, const pt_camera* cam, uint32_t spp, uint
     }
     P.tileCursor = ctx->tileCursor;
     P.numSlots = tiles;
-    if (stats) PT_HIP_CHECK(ctx, hipMemsetAsync(ctx->stats, 0, 16 * sizeof(unsigned long long), ctx->stream));
+    P.occCap = ctx->occupancy;
+    if (stats) PT_HIP_CHECK(ctx, hipMemsetAsync(ctx->stats, 0, kStatWords * sizeof(unsigned long long), ctx->stream));
     int variant = pick_variant(ctx);
     // speculative sample groups
     const uint32_t total = spp * chunks;
@@ -2630,6 +2694,7 @@ static int render_impl(pt_context* ctx, const pt_camera* cam, uint32_t spp, uint
                          (size_t)tiles * J * ssg_window_words(G, ssgN)))
             G = 0;
     }
+    if (!G) ssg_release(ctx);
     if (G && P.tileCost) PT_HIP_CHECK(ctx, hipMemsetAsync(P.tileCost, 0, (size_t)tiles * sizeof(uint32_t), ctx->stream));
     if (G) {
         const int rc = run_groups(ctx, variant, P, G, tiles, ssgCap, ctx->stream);
@@ -2649,7 +2714,7 @@ static int render_impl(pt_context* ctx, const pt_camera* cam, uint32_t spp, uint
         if (rs != PT_OK) return rs;
     }
     if (stats) {
-        unsigned long long h[16];
+        unsigned long long h[kStatWords];
         PT_HIP_CHECK(ctx, hipMemcpy(h, ctx->stats, sizeof(h), hipMemcpyDeviceToHost));
         stats->node_tests = h[0];
         stats->prim_tests = h[1];
@@ -2667,6 +2732,9 @@ static int render_impl(pt_context* ctx, const pt_camera* cam, uint32_t spp, uint
         stats->cycles_shading = h[13];
         stats->cycles_total = h[14];
         stats->cycles_lane_idle = h[15];
+        stats->leaf_rounds = h[16];
+        stats->family_execs = h[17];
+        stats->family_execs_compacted = h[18];
     }
     return PT_OK;
 }
@@ -2717,6 +2785,13 @@ PT_API int pt_read_group_stats(const pt_context* ctx, uint32_t* dst)
 {
     if (!ctx || !dst) return PT_ERR_ARG;
     memcpy(dst, ctx->groupStats, sizeof(ctx->groupStats));
+    return PT_OK;
+}
+
+PT_API int pt_set_occupancy(pt_context* ctx, uint32_t workgroups_per_cu)
+{
+    if (!ctx || workgroups_per_cu > 16) return PT_ERR_ARG;
+    ctx->occupancy = workgroups_per_cu;
     return PT_OK;
 }
 

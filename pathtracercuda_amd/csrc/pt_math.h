@@ -32,29 +32,27 @@ constexpr float kFltMax = 3.402823466e+38f;
 // square root for 2^-96 <= x <= FLT_MAX (profiles/r01_fp_exhaustive.json: 0 mismatches).  Other inputs
 // (zero, denormals, huge values, inf, NaN) take the general path.  Being correctly rounded, both
 // give exactly IEEE 1/x and sqrt(x) -- the oracle's and the reference's values.
-// Guard form used by every helper below: the fast sequence runs for all lanes, and only lanes
-// outside its range take a divergent fix-up region that overwrites the result with the general
-// expression.  One region (usually skipped whole: exec is zero) instead of an if/else pair -- fewer
-// exec-mask operations on the CU's scalar unit and no value held across two regions (the if/else
-// form made the register allocator spill shading temporaries around the branches).  Values are
-// unchanged: each lane's result is the fast sequence's in range and the general one outside.
 PT_DEV float rcp_rn(float x)
 {
-    const float y = __builtin_amdgcn_rcpf(x);
-    float r = __builtin_fmaf(__builtin_fmaf(-x, y, 1.0f), y, y);
     const float ax = __builtin_fabsf(x);
-    if (!(ax >= 0x1p-125f && ax <= 0x1p125f)) r = 1.0f / x;
-    return r;
+    if (ax >= 0x1p-125f && ax <= 0x1p125f) {
+        const float y = __builtin_amdgcn_rcpf(x);
+        const float e = __builtin_fmaf(-x, y, 1.0f);
+        return __builtin_fmaf(e, y, y);
+    }
+    return 1.0f / x;
 }
 
 PT_DEV float sqrt_rn(float x)
 {
-    const float y = __builtin_amdgcn_rsqf(x);              // ~1/sqrt(x)
-    const float s0 = x * y, h = 0.5f * y;
-    float s = __builtin_fmaf(__builtin_fmaf(-s0, s0, x), h, s0);   // exact residual x - s0^2
     // one unsigned compare: 2^-96 <= x <= FLT_MAX (negatives, inf and NaN fall outside)
-    if (!(__float_as_uint(x) - 0x0f800000u <= 0x7f7fffffu - 0x0f800000u)) s = sqrtf(x);
-    return s;
+    if (__float_as_uint(x) - 0x0f800000u <= 0x7f7fffffu - 0x0f800000u) {
+        const float y = __builtin_amdgcn_rsqf(x);          // ~1/sqrt(x)
+        const float s0 = x * y, h = 0.5f * y;
+        const float r = __builtin_fmaf(-s0, s0, x);        // exact residual x - s0^2
+        return __builtin_fmaf(r, h, s0);
+    }
+    return sqrtf(x);
 }
 
 // Two roots, or a root and its reciprocal, behind ONE range guard (each divergent guard costs the
@@ -76,19 +74,19 @@ PT_DEV float sqrt_fast(float x)
 }
 PT_DEV void sqrt2_rn(float a, float b, float& sa, float& sb)
 {
-    sa = sqrt_fast(a);
-    sb = sqrt_fast(b);
-    if (!(sqrt_fast_ok(a) && sqrt_fast_ok(b))) {
-        sa = sqrtf(a);
-        sb = sqrtf(b);
+    if (sqrt_fast_ok(a) && sqrt_fast_ok(b)) {
+        sa = sqrt_fast(a);
+        sb = sqrt_fast(b);
+    } else {
+        sa = sqrt_rn(a);
+        sb = sqrt_rn(b);
     }
 }
 // 1 / sqrt_rn(x): a root in sqrt's fast range lies in [2^-48, 2^64], inside rcp's fast range
 PT_DEV float rcp_sqrt_rn(float x)
 {
-    float r = rcp_fast(sqrt_fast(x));
-    if (!sqrt_fast_ok(x)) r = 1.0f / sqrtf(x);
-    return r;
+    if (sqrt_fast_ok(x)) return rcp_fast(sqrt_fast(x));
+    return rcp_rn(sqrtf(x));
 }
 
 // The same values with the guard as a wave-uniform branch: the fast sequence runs for every
@@ -132,11 +130,13 @@ PT_DEV float div_const(float x)
 {
     constexpr float c = K == 1 ? 3.14159265358979323846f : 2.0f * 3.14159265358979323846f;
     constexpr float y = 1.0f / c;                    // RN(1/c), folded at compile time
-    const float q = x * y;
-    float r = __builtin_fmaf(__builtin_fmaf(-c, q, x), y, q);
     const float ax = __builtin_fabsf(x);
-    if (!(ax >= 0x1p-100f && ax <= 0x1p100f)) r = x / c;
-    return r;
+    if (ax >= 0x1p-100f && ax <= 0x1p100f) {
+        const float q = x * y;
+        const float r = __builtin_fmaf(-c, q, x);
+        return __builtin_fmaf(r, y, q);
+    }
+    return x / c;
 }
 PT_DEV float div_pi(float x) { return div_const<1>(x); }
 PT_DEV float div_two_pi(float x) { return div_const<2>(x); }
@@ -162,12 +162,16 @@ PT_DEV float length(f3 v) { return sqrt_rn(v.x * v.x + v.y * v.y + v.z * v.z); }
 PT_DEV f3 normalize(f3 v)
 {
     const float l2 = v.x * v.x + v.y * v.y + v.z * v.z;
-    const float y = __builtin_amdgcn_rsqf(l2);
-    const float s0 = l2 * y, h = 0.5f * y;
-    const float l = __builtin_fmaf(__builtin_fmaf(-s0, s0, l2), h, s0);
-    const float r = __builtin_amdgcn_rcpf(l);
-    float inv = __builtin_fmaf(__builtin_fmaf(-l, r, 1.0f), r, r);
-    if (!(__float_as_uint(l2) - 0x0f800000u <= 0x7f7fffffu - 0x0f800000u)) inv = rcp_rn(sqrtf(l2));
+    float inv;
+    if (__float_as_uint(l2) - 0x0f800000u <= 0x7f7fffffu - 0x0f800000u) {
+        const float y = __builtin_amdgcn_rsqf(l2);
+        const float s0 = l2 * y, h = 0.5f * y;
+        const float l = __builtin_fmaf(__builtin_fmaf(-s0, s0, l2), h, s0);
+        const float r = __builtin_amdgcn_rcpf(l);
+        inv = __builtin_fmaf(__builtin_fmaf(-l, r, 1.0f), r, r);
+    } else {
+        inv = rcp_rn(sqrtf(l2));
+    }
     return scale(inv, v);
 }
 PT_DEV f3 reflect(f3 v, f3 n) { return sub(v, scale(2.0f * dot(v, n), n)); }

@@ -97,3 +97,21 @@ def test_groups_refused_beyond_the_fold_word(gpu_available, scenes):
     b.render(cam, 1, True, chunks=chunks)
     assert np.array_equal(a.accum().view(np.uint32), b.accum().view(np.uint32))
     assert np.array_equal(a.rng_state(), b.rng_state())
+
+
+def test_groups_after_plain_launch_reallocate(gpu_available, scenes):
+    # a plain launch releases the group logs (pt_kernels.hip ssg_release); a later grouped launch
+    # allocates them again and still reproduces the plain sequence bit for bit
+    W, H = 96, 54
+    a = pa.Pathtracer(W, H)
+    cam = a.load_scene(str(scenes / "generated_scene.scene.json"))
+    b = pa.Pathtracer(W, H)
+    b.load_scene(str(scenes / "generated_scene.scene.json"))
+    b.set_sample_groups(1)
+    for mode, ignore in ((4, True), (1, False), (4, False)):
+        a.set_sample_groups(mode)
+        a.render(cam, 8, ignore, chunks=16)
+        assert a.last_sample_groups == (4 if mode == 4 else 0)
+        b.render(cam, 8, ignore, chunks=16)
+        same(a.accum(), b.accum(), f"groups {mode}")
+        assert np.array_equal(a.rng_state(), b.rng_state())

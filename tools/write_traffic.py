@@ -25,7 +25,11 @@ def main():
         merged.update({k: v for k, v in c.items() if k != "DURATION_NS"})
         merged.setdefault("duration_ns", c.get("DURATION_NS"))
     fetch, write = merged.get("FETCH_SIZE"), merged.get("WRITE_SIZE")
-    out = {"workload": workload, "kernel": "trace_kernel (timed launch)",
+    sha = (src / "kernel_sha.txt").read_text().strip() if (src / "kernel_sha.txt").exists() else None
+    head = subprocess.run(["git", "-C", str(ROOT), "rev-parse", "--short", "HEAD"], capture_output=True,
+                          text=True).stdout.strip()
+    out = {"workload": workload, "kernel": "trace_kernel (timed launch)", "kernel_sha": sha,
+           "commit": (sys.argv[4] if len(sys.argv) > 4 else head),
            "fetch_size_kib": fetch, "write_size_kib": write,
            "bytes_per_launch": (2 * fetch + write) * 1024 if fetch is not None and write is not None else None,
            "correction": "FETCH_SIZE x2 (gfx950 reports half of wide coalesced reads); KiB -> bytes",
