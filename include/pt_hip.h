@@ -200,6 +200,10 @@ PT_API int pt_set_schedule(pt_context *ctx, int mode);
  * fit, the default).  Results are identical. */
 PT_API int pt_set_occupancy(pt_context *ctx, uint32_t workgroups_per_cu);
 
+/* Issue priority of the most expensive tiles: waves rendering the first `slots` positions of the
+ * cost order run at raised wave priority (s_setprio).  -1 = automatic (default), 0 = off. */
+PT_API int pt_set_priority_slots(pt_context *ctx, int slots);
+
 /* Speculative sample groups.  A pixel's samples are one serial XORWOW stream
  * (trace.cu:183-193), so a launch with fewer 8x8 tiles than about four per wave slot of the chip
  * (multi-GPU strong scaling, small images) lasts as long as its slowest tile's whole chain.  With

@@ -305,6 +305,12 @@ class Pathtracer:
         for c in self._contexts():
             N.check_ctx(N.hip().pt_set_occupancy(c, int(workgroups_per_cu)), c)
 
+    def set_priority_slots(self, slots: int) -> None:
+        """Waves on the first `slots` positions of the cost order run at raised issue priority
+        (pt_set_priority_slots; -1 = automatic, 0 = off).  Results are identical."""
+        for c in self._contexts():
+            N.check_ctx(N.hip().pt_set_priority_slots(c, int(slots)), c)
+
     def set_schedule(self, mode: int) -> None:
         """0 = cost-sorted tile dispatch (default), 1 = row-major (pt_set_schedule), every device."""
         for c in self._contexts():

@@ -104,6 +104,7 @@ struct TraceParams {
     uint32_t* fold;             // [kFoldWords][rows*width] fold state (ssg_fold_kernel); AUX resume input
     DevCamera cam;
     uint32_t occCap;            // host only: persistent grids hold at most this many workgroups per CU (0 = all)
+    uint32_t prioSlots;         // waves on order positions < prioSlots run at raised issue priority
 };
 
 // Speculative sample groups: window of a group's start offset in which an earlier group's parse can
@@ -1081,14 +1082,16 @@ PT_DEV void flush_counters(const TraceParams& P, const Counters& cnt)
     atomicAdd(&P.stats[18], (unsigned long long)cnt.w_fam_ideal);
 }
 
-// One atomic per wave: the first active lane adds n to *cursor and broadcasts the old value.
+// One atomic per wave: the first active lane adds n to *cursor; the old value is read back from
+// that lane into a scalar register (readfirstlane), so the slot and everything derived from it --
+// tile, pixel base, priority -- is wave-uniform for the compiler too (SGPRs, scalar loads).
 PT_DEV uint32_t wave_fetch(uint32_t* cursor, uint32_t n)
 {
     const unsigned long long m = __ballot(1);
     const uint32_t leader = (uint32_t)(__ffsll((long long)m) - 1);
     uint32_t base = 0;
     if ((threadIdx.x & 63u) == leader) base = atomicAdd(cursor, n);
-    return (uint32_t)__shfl((int)base, (int)leader, 64);
+    return __builtin_amdgcn_readfirstlane(base);
 }
 
 // ---------------------------------------------------------------------------------------------
@@ -1369,7 +1372,7 @@ __global__ void __launch_bounds__(WPB * 64, MINW) trace_kernel(TraceParams P)
     uint32_t* stack = ldsStacks + wave * stackWords + (WW >= 3 ? 2u : 1u) * lane;
     const uint32_t accL = 4u * sceneF4 + WPB * stackWords + wave * 192u + lane;   // float index
     Counters cnt = {};
-    uint32_t slot = PERSIST ? wave_fetch(P.tileCursor, 1u) : blockIdx.x * (uint32_t)WPB + wave;
+    uint32_t slot = PERSIST ? wave_fetch(P.tileCursor, 1u) : __builtin_amdgcn_readfirstlane(blockIdx.x * (uint32_t)WPB + wave);
     for (;;) {
     if (slot >= P.numSlots) break;               // also the grid's spare slots past the last item
     uint32_t tile, grp = 0, pos = slot;              // pos: the tile's position in the order
@@ -1379,6 +1382,12 @@ __global__ void __launch_bounds__(WPB * 64, MINW) trace_kernel(TraceParams P)
         grp = slot - pos * J;                        // item within the tile (ssg_load)
     }
     tile = P.order ? P.order[pos] : pos;          // packed coordinates (scatter mode: wave index)
+    // Issue priority: the cost order puts the most expensive tiles first, and at full occupancy
+    // such a tile's chain runs ~3x slower than alone (tools/occupancy_probe.py) -- long enough to
+    // end the launch.  Waves on the first prioSlots positions take issue slots first (s_setprio),
+    // the others fill the gaps.  Scheduling only: results are identical.
+    if (pos < P.prioSlots) __builtin_amdgcn_s_setprio(3);
+    else __builtin_amdgcn_s_setprio(0);
     const PixelCtx pc = pixel_of(P, tile, lane);
     const uint64_t tWave = __builtin_amdgcn_s_memtime();
     const bool run = pc.valid && (!AUX || !P.fold || (P.fold[F_FLAG * pc.npix + pc.li] & 1u));
@@ -1882,6 +1891,7 @@ struct pt_context {
     bool orderStale = true;       // rebuild it after the next launch (scene, texture or camera changed)
     int schedule = 0;             // 0 = cost-sorted tiles (default), 1 = row-major
     uint32_t occupancy = 0;       // tuning knob: workgroups per CU of persistent grids (0 = all that fit)
+    int prioSlots = -1;           // order positions run at raised issue priority (-1 = automatic)
     // speculative sample groups
     int ssgMode = 0;              // 0 = automatic, 1 = off, G >= 2 = always G groups (tests)
     uint32_t patchRounds = 6;     // patch rounds before the remaining dead ends run plain
@@ -2642,6 +2652,7 @@ static int render_impl(pt_context* ctx, const pt_camera* cam, uint32_t spp, uint
     P.tileCursor = ctx->tileCursor;
     P.numSlots = tiles;
     P.occCap = ctx->occupancy;
+    P.prioSlots = ctx->prioSlots >= 0 ? (uint32_t)ctx->prioSlots : 0u;
     if (stats) PT_HIP_CHECK(ctx, hipMemsetAsync(ctx->stats, 0, kStatWords * sizeof(unsigned long long), ctx->stream));
     int variant = pick_variant(ctx);
     // speculative sample groups
@@ -2785,6 +2796,13 @@ PT_API int pt_read_group_stats(const pt_context* ctx, uint32_t* dst)
 {
     if (!ctx || !dst) return PT_ERR_ARG;
     memcpy(dst, ctx->groupStats, sizeof(ctx->groupStats));
+    return PT_OK;
+}
+
+PT_API int pt_set_priority_slots(pt_context* ctx, int slots)
+{
+    if (!ctx || slots < -1) return PT_ERR_ARG;
+    ctx->prioSlots = slots;
     return PT_OK;
 }
 
