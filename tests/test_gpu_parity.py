@@ -146,6 +146,28 @@ def test_tile_schedule_does_not_change_results(gpu_available, scenes):
         assert np.array_equal(sorted_rng, ref.rng_array())
 
 
+def test_schedule_knobs_do_not_change_results(gpu_available, scenes):
+    # issue priority for the head of the cost order, CU-masked split launches (the head on reserved
+    # CUs at low occupancy), occupancy caps: only which wave renders a tile and when changes
+    W, H = 1280, 720
+    pt = pa.Pathtracer(W, H)
+    cam = pt.load_scene(scenes / "generated_scene.scene.json")
+    st = pt.rng_state()
+    pt.render(cam, 8, True, chunks=2)                 # cost order
+    pt.set_rng_state(st)
+    pt.render(cam, 4, True, chunks=3)
+    want = pt.accum().view(np.uint32).copy()
+    want_rng = pt.rng_state()
+    for prio, res, occ in [(64, (0, 1, 0), 0), (0, (16, 1, 0), 0), (256, (32, 2, 300), 0), (0, (0, 1, 0), 2)]:
+        pt.set_priority_slots(prio)
+        pt.set_reserved_cus(*res)
+        pt.set_occupancy(occ)
+        pt.set_rng_state(st)
+        pt.render(cam, 4, True, chunks=3)
+        assert np.array_equal(pt.accum().view(np.uint32), want), (prio, res, occ)
+        assert np.array_equal(pt.rng_state(), want_rng), (prio, res, occ)
+
+
 def test_fast_reciprocal_and_sqrt_exhaustive(gpu_available, root):
     # pt::rcp_rn / pt::sqrt_rn (pt_math.h) against hipcc's correctly rounded 1.0f/x and sqrtf(x)
     # for every one of the 2^32 float inputs

@@ -1,0 +1,68 @@
+"""Launch time of one workload under several tile schedules, interleaved rounds in one process,
+results checked bit-identical against the first schedule.  A schedule is a comma-free token:
+    p<K>                 issue priority for the first K positions of the cost order (pt_set_priority_slots)
+    r<R>w<W>[k<K>]       split launch: the first K positions (default one per reserved wave slot) on R
+                         reserved CUs at W waves per SIMD, the rest on the other CUs (pt_set_reserved_cus)
+    r<R>w<W>k<K>p<P>     both
+Usage on the GPU box:
+    python tools/sched_probe.py [--width 1920 --height 1080 --spp 1024 --n 1] --scheds p0,p256,r16w1,r32w2k256
+"""
+import argparse
+import json
+import pathlib
+import re
+import sys
+
+import numpy as np
+
+ROOT = pathlib.Path(__file__).resolve().parents[1]
+sys.path.insert(0, str(ROOT))
+import pathtracercuda_amd as pa  # noqa: E402
+
+
+def apply(pt, tok):
+    m = re.fullmatch(r"(?:r(\d+)w(\d+)(?:k(\d+))?)?(?:p(\d+))?", tok)
+    if not m:
+        raise SystemExit(f"bad schedule {tok}")
+    r, w, k, p = m.groups()
+    pt.set_reserved_cus(int(r or 0), int(w or 1), int(k or 0))
+    pt.set_priority_slots(int(p or 0))
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--scene", default=str(ROOT / "scenes/generated_scene.scene.json"))
+    ap.add_argument("--width", type=int, default=1920)
+    ap.add_argument("--height", type=int, default=1080)
+    ap.add_argument("--spp", type=int, default=1024)
+    ap.add_argument("--n", type=int, default=1, help="rank 0's share of an N-way 8-row band partition")
+    ap.add_argument("--scheds", default="p0,p256")
+    ap.add_argument("--rounds", type=int, default=3)
+    ap.add_argument("--groups", type=int, default=1, help="sample groups: 1 = off, 0 = automatic")
+    a = ap.parse_args()
+    pt = (pa.Pathtracer(a.width, a.height, row_offset=0, row_stride=a.n, band_rows=8) if a.n > 1
+          else pa.Pathtracer(a.width, a.height))
+    pt.set_sample_groups(a.groups)
+    cam = pt.load_scene(a.scene)
+    st = pt.rng_state()
+    pt.render_raw(cam, 8, 2, True)                      # cost order
+    scheds = a.scheds.split(",")
+    times = {k: [] for k in scheds}
+    ref = None
+    for r in range(a.rounds):
+        for k in (scheds if r % 2 == 0 else scheds[::-1]):
+            apply(pt, k)
+            pt.set_rng_state(st)
+            times[k].append(pt.render_raw(cam, 8, a.spp // 8, True))
+            acc = pt.accum().view(np.uint32)
+            if ref is None:
+                ref = acc.copy()
+            assert np.array_equal(acc, ref), f"{k}: results differ"
+    tiles = ((a.width + 7) // 8) * ((pt.rows + 7) // 8)
+    print(json.dumps({"image": f"{a.width}x{a.height}", "n": a.n, "spp": a.spp, "tiles": tiles,
+                      "groups": pt.last_sample_groups, "ms_min": {k: round(min(v), 2) for k, v in times.items()},
+                      "ms_all": {k: [round(x, 2) for x in v] for k, v in times.items()}}), flush=True)
+
+
+if __name__ == "__main__":
+    main()
