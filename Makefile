@@ -17,7 +17,11 @@ HOST_SRCS := $(SRC)/host/math_camera.cpp $(SRC)/host/hittable.cpp $(SRC)/host/bv
              $(SRC)/host/renderer.cpp $(SRC)/host/host_capi.cpp
 HOST_HDRS := include/pathtracer_amd.hpp include/pt_host.h include/pt_hip.h $(SRC)/host/host_internal.h $(SRC)/host/json_min.h
 
-HIPFLAGS ?= --offload-arch=$(ARCH) -O3 -std=c++17 -ffp-contract=off -fPIC -fvisibility=hidden \
+# -fno-slp-vectorize: the kernel's packed FP32 pairs are written out (ext_vector_type); the SLP
+# vectorizer's own pairings bound two scalars of the GGX visibility term into one register tuple
+# that the allocator then spilled around a range guard in every GGX shading.  Off: scratch 40 -> 12
+# B/lane (no spill inside the loop), +4.6 % on C3 same-box (profiles/r03_slp_ab.json).
+HIPFLAGS ?= --offload-arch=$(ARCH) -O3 -std=c++17 -ffp-contract=off -fno-slp-vectorize -fPIC -fvisibility=hidden \
             -mcode-object-version=5 -Iinclude -Wall -Wno-unused-result
 CXXFLAGS ?= -O2 -std=c++17 -ffp-contract=off -fno-fast-math -fPIC -Iinclude -I$(SRC)/host -Wall -Wextra \
             -Wno-unused-parameter -Wno-missing-field-initializers
