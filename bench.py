@@ -18,11 +18,15 @@ N GPUs, two launch modes, one partition (8-row bands, band b -> GPU b mod N):
     (pt_group_*: one context and host thread per GPU, ncclCommInitAll, grouped ncclSend/ncclRecv +
     unpermute kernel -- the boundary that replaces Pathtracer.cpp:40's single device); the timed
     step is pt_group_render + pt_group_gather.  Fewer than N visible GPUs is an error (exit 2);
-    `--group 1` runs this path at N = 1 too.  Default: strong scaling (the
-same workload for every N); `--scaling weak` grows the image by sqrt(N) per axis instead.  At N > 1
-a short weak-scaling measurement is added as a secondary field; at N = 1 the C2 and C5 workloads are
-added as secondary records, each with its roofline and CPU baseline (`--extra ''` drops C5,
-`--secondary 0` turns all of them off).
+    `--group 1` runs this path at N = 1 too.
+Scaling.  The path is partitioned (pixels are independent; the only exchange is the one framebuffer
+gather), so the headline is weak scaling (the task's rule for partitioned paths): every
+GPU keeps one C3 frame's worth of pixels -- the image grows by sqrt(N) per axis (N = 4: 3840x2160,
+C4's image, at 1024 spp) -- and value = all samples / step time.  At N > 1 a strong-scaling record
+of the fixed 1920x1080 image is added beside it (`secondary`), so both are on the driver's clock;
+`--scaling strong` makes the fixed image the headline.  At N = 1 the two coincide, and the C2 and C5
+workloads are added as secondary records, each with its roofline and CPU baseline (`--extra ''` drops
+C5, `--secondary 0` turns all secondary records off).
 
 Printed JSON line (rank 0): value = samples of the whole workload / step time.  roofline: the
 trace kernel is bound by VALU issue -- achieved = its wave64 VALU instructions per
@@ -70,10 +74,11 @@ def parse_args(argv=None):
     p.add_argument("--warmup", type=int, default=1)
     p.add_argument("--config", choices=sorted(CONFIGS), default="C3")
     p.add_argument("--spp", type=int, default=0, help="override the config's spp (multiple of 8)")
-    p.add_argument("--scaling", choices=["weak", "strong"], default="strong",
+    p.add_argument("--scaling", choices=["weak", "strong"], default="weak",
                    help="strong: the same workload for every N (default); weak: the image grows by sqrt(N) per axis")
     p.add_argument("--band-rows", type=int, default=8, help="rows per band of the multi-GPU partition")
-    p.add_argument("--secondary", type=int, default=1, help="N=1: add the C2 record; N>1: add a weak-scaling record")
+    p.add_argument("--secondary", type=int, default=1,
+                   help="N=1: add the C2 and --extra records; N>1: add the other scaling mode's record")
     p.add_argument("--cpu-baseline", type=int, default=1, help="time the oracle on a bounded sample (rank 0, N=1)")
     p.add_argument("--cpu-seconds", type=float, default=15.0, help="target length of the CPU baseline run")
     p.add_argument("--cpu-threads", type=int, default=0, help="0 = every core this process may use")
@@ -467,16 +472,20 @@ def main():
                     rec2["cpu_baseline"] = cpu_baseline(args, c2, c2["width"], c2["height"])
                 recs.append(rec2)
             out["secondary"] = recs
-        elif args.scaling == "strong":
-            Ww = int(round(cfg["width"] * math.sqrt(n) / 8.0)) * 8
-            Hw = int(round(cfg["height"] * math.sqrt(n) / 8.0)) * 8
+        else:
+            other = "strong" if args.scaling == "weak" else "weak"
+            Ww, Hw = cfg["width"], cfg["height"]
+            if other == "weak":
+                Ww = int(round(cfg["width"] * math.sqrt(n) / 8.0)) * 8
+                Hw = int(round(cfg["height"] * math.sqrt(n) / 8.0)) * 8
             rw = Run(cfg, Ww, Hw, spp, rank, n, local_rank, args.band_rows, mode)
             stw = stats_all(rw.instrument())
             ew, kw = timed(rw, min(args.steps, 3), 1, local_rank, dist_on)
             recw = record(cfg, rw, ew, kw, min(args.steps, 3), stw, n)
             rw.close()
-            recw["label"] = f"{args.config} weak scaling (image {Ww}x{Hw}: one {cfg['width']}x{cfg['height']} frame per GPU)"
-            recw["scaling"] = "weak"
+            recw["label"] = (f"{args.config} weak scaling (image {Ww}x{Hw}: one {cfg['width']}x{cfg['height']} frame per GPU)"
+                             if other == "weak" else f"{args.config} strong scaling (the fixed {Ww}x{Hw} image on {n} GPUs)")
+            recw["scaling"] = other
             out["secondary"] = [recw]
     if rank == 0 and n == 1 and args.cpu_baseline:
         out["cpu_baseline"] = cpu_baseline(args, cfg, W, H)
