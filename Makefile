@@ -60,3 +60,7 @@ clean:
 	$(MAKE) -C oracle clean
 
 .PHONY: all oracle clean sanitize
+
+# `make -s print-HIPFLAGS`: the flags snapshot builds (tools/snap_rev.sh) reuse
+print-%:
+	@echo $($*)

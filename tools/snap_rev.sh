@@ -13,8 +13,8 @@ cp pathtracercuda_amd/*.py "$d/pathtracercuda_amd/"
 cp pathtracercuda_amd/lib/libpt_host.so "$d/pathtracercuda_amd/lib/"
 cp tools/ab_variants.py tools/one_launch.py "$d/tools/"
 cp -r scenes "$d/"
-/opt/rocm/bin/hipcc --offload-arch=gfx950 -O3 -std=c++17 -ffp-contract=off -fPIC -fvisibility=hidden \
-  -mcode-object-version=5 -I"$src/include" -Wall -Wno-unused-result $flags -shared \
+base=$(make -s print-HIPFLAGS | sed 's/-Iinclude//')
+/opt/rocm/bin/hipcc $base -I"$src/include" $flags -shared \
   -o "$d/pathtracercuda_amd/lib/libpt_hip.so" "$src/pathtracercuda_amd/csrc/pt_kernels.hip" -lrccl
 rm -rf "$src"
 echo "built $d from $rev ($flags)"
