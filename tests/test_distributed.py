@@ -61,7 +61,7 @@ def test_band_partition_covers_image_once(band):
     # every image row belongs to exactly one rank; the Python partition, the native one
     # (pt_band_rows, libpt_hip.so) and the oracle's (or_view_rows) agree
     from pathtracercuda_amd import _native as N
-    for H in (1, 7, 8, 9, 64, 1080, 2160):
+    for H in (1, 7, 8, 9, 64, 1080, 1528, 2160, 3056):
         for world in (1, 2, 3, 8):
             seen = []
             for r in range(world):
