@@ -434,6 +434,18 @@ def test_edge_cases(gpu_available, scenes):
     assert not empty.accum().any()
 
 
+def test_context_size_limits(gpu_available):
+    # tiles are addressed by packed 16-bit coordinates and pixels by 32-bit indices: contexts beyond
+    # that are refused with an error, never created with wrapped indices
+    with pytest.raises(pa.PathtracerError):
+        pa.Pathtracer(32768, 32768)                  # 2^30 pixels
+    with pytest.raises(pa.PathtracerError):
+        pa.Pathtracer(8 * 65536, 8)                  # 65,536 tiles across
+    pt = pa.Pathtracer(8 * 65535, 8)                 # the widest accepted image
+    assert pt.rows == 8
+    pt.close()
+
+
 def test_full_resolution_row_subset(gpu_available, scenes):
     # BASELINE config C3 geometry (1920x1080, generated_scene + sky): exact parity on every 45th row
     W, H, stride = 1920, 1080, 45
