@@ -48,12 +48,18 @@ def main():
     pt.render_raw(cam, 8, 2, True)                      # cost order
     scheds = a.scheds.split(",")
     times = {k: [] for k in scheds}
+    tails = {k: [] for k in scheds}
+    order = None
     ref = None
     for r in range(a.rounds):
         for k in (scheds if r % 2 == 0 else scheds[::-1]):
             apply(pt, k)
             pt.set_rng_state(st)
             times[k].append(pt.render_raw(cam, 8, a.spp // 8, True))
+            cost = pt.tile_costs().ravel().astype(np.float64) / 2.4e6          # ms at 2.4 GHz
+            if order is None:
+                order = np.argsort(-cost)[: max(1, cost.size // 100)]          # the first schedule's top 1 %
+            tails[k].append((float(cost.max()), float(cost[order].mean()), float(cost.mean())))
             acc = pt.accum().view(np.uint32)
             if ref is None:
                 ref = acc.copy()
@@ -61,7 +67,9 @@ def main():
     tiles = ((a.width + 7) // 8) * ((pt.rows + 7) // 8)
     print(json.dumps({"image": f"{a.width}x{a.height}", "n": a.n, "spp": a.spp, "tiles": tiles,
                       "groups": pt.last_sample_groups, "ms_min": {k: round(min(v), 2) for k, v in times.items()},
-                      "ms_all": {k: [round(x, 2) for x in v] for k, v in times.items()}}), flush=True)
+                      "ms_all": {k: [round(x, 2) for x in v] for k, v in times.items()},
+                      "tile_ms_max_top1pct_mean": {k: [round(float(np.mean([t[i] for t in v])), 2) for i in range(3)]
+                                                   for k, v in tails.items()}}), flush=True)
 
 
 if __name__ == "__main__":
