@@ -1891,6 +1891,7 @@ struct pt_context {
     uint32_t orderTiles = 0;      // tiles the device buffers hold
     bool orderValid = false;      // `order` holds a cost-sorted permutation
     bool orderStale = true;       // rebuild it after the next launch (scene, texture or camera changed)
+    uint64_t orderSamples = 0;    // samples per pixel of the launch whose tile costs built `order`
     int schedule = 0;             // 0 = cost-sorted tiles (default), 1 = row-major
     uint32_t occupancy = 0;       // tuning knob: workgroups per CU of persistent grids (0 = all that fit)
     int prioSlots = -1;           // order positions run at raised issue priority (-1 = automatic)
@@ -2484,8 +2485,9 @@ static void ssg_release(pt_context* ctx)
 
 // Stable radix sort of (cost, tile) pairs, descending, into the dispatch order: deterministic, ties
 // in tile order.
-static int sort_order(pt_context* ctx, uint32_t tiles)
+static int sort_order(pt_context* ctx, uint32_t tiles, uint64_t samples)
 {
+    ctx->orderSamples = samples;
     size_t bytes = ctx->sortTempBytes;
     PT_HIP_CHECK(ctx, rocprim::radix_sort_pairs_desc(ctx->sortTemp, bytes, ctx->tileCost, ctx->sortKeys, ctx->tileIds,
                                                      ctx->order, tiles, 0, 32, ctx->stream));
@@ -2749,7 +2751,7 @@ static int render_impl(pt_context* ctx, const pt_camera* cam, uint32_t spp, uint
         Q.pairsOut = guesses && ssg_reserve(ctx, tiles, 0, 0, 0) ? ctx->pairs : nullptr;
         if (Q.pairsOut) ctx->pairsValid = true;
         PT_HIP_CHECK(ctx, Q.pairsOut ? launch_grouped<2>(variant, Q, ctx->stream) : launch_variant<false>(variant, Q, ctx->stream));
-        const int rs = sort_order(ctx, tiles);
+        const int rs = sort_order(ctx, tiles, Q.spp);
         if (rs != PT_OK) return rs;
         P.order = ctx->order;
     }
@@ -2782,8 +2784,12 @@ static int render_impl(pt_context* ctx, const pt_camera* cam, uint32_t spp, uint
     float ms = 0.0f;
     PT_HIP_CHECK(ctx, hipEventElapsedTime(&ms, ctx->ev0, ctx->ev1));
     if (gpu_ms) *gpu_ms = ms;
-    if (sorted && (ctx->orderStale || !ctx->orderValid)) {
-        const int rs = sort_order(ctx, tiles);
+    // The order is rebuilt from this launch's tile costs when it is stale, or when this launch
+    // measured every tile over at least 4x as many samples as the costs the order came from (a cold
+    // start's 2-spp pre-pass, an 8-spp first launch): short launches rank tiles noisily, and a heavy
+    // tile ranked light is dispatched late and becomes the launch's tail.
+    if (sorted && (ctx->orderStale || !ctx->orderValid || total >= 4 * ctx->orderSamples)) {
+        const int rs = sort_order(ctx, tiles, total);
         if (rs != PT_OK) return rs;
     }
     if (stats) {
