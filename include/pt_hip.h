@@ -200,9 +200,10 @@ PT_API int pt_set_schedule(pt_context *ctx, int mode);
  * fit, the default).  Results are identical. */
 PT_API int pt_set_occupancy(pt_context *ctx, uint32_t workgroups_per_cu);
 
-/* Issue priority of the most expensive tiles: waves rendering the first `slots` positions of the
- * cost order run at raised wave priority (s_setprio).  -1 = automatic (default), 0 = off. */
-PT_API int pt_set_priority_slots(pt_context *ctx, int slots);
+/* Issue priority by position in the cost order (s_setprio): mode 0 = automatic (default), 1 = off,
+ * 2 = explicit -- positions < level3 run at wave priority 3, < level2 at 2, < level1 at 1, the
+ * rest at 0 (level3 <= level2 <= level1).  Results are identical. */
+PT_API int pt_set_issue_priority(pt_context *ctx, int mode, uint32_t level3, uint32_t level2, uint32_t level1);
 
 /* Split launches (measurement knob, 0 CUs = off, the default): the first `tiles` positions of the
  * cost order (0 = one per reserved wave slot) render on `cus` CUs at `waves_per_simd` waves per SIMD

@@ -305,11 +305,12 @@ class Pathtracer:
         for c in self._contexts():
             N.check_ctx(N.hip().pt_set_occupancy(c, int(workgroups_per_cu)), c)
 
-    def set_priority_slots(self, slots: int) -> None:
-        """Waves on the first `slots` positions of the cost order run at raised issue priority
-        (pt_set_priority_slots; -1 = automatic, 0 = off).  Results are identical."""
+    def set_issue_priority(self, mode: int, level3: int = 0, level2: int = 0, level1: int = 0) -> None:
+        """Issue priority by cost-order position (pt_set_issue_priority): mode 0 automatic, 1 off,
+        2 explicit (positions < level3 at priority 3, < level2 at 2, < level1 at 1).  Results are
+        identical."""
         for c in self._contexts():
-            N.check_ctx(N.hip().pt_set_priority_slots(c, int(slots)), c)
+            N.check_ctx(N.hip().pt_set_issue_priority(c, int(mode), int(level3), int(level2), int(level1)), c)
 
     def set_reserved_cus(self, cus: int, waves_per_simd: int = 1, tiles: int = 0) -> None:
         """Split launches (pt_set_reserved_cus): the head of the cost order on `cus` reserved CUs at

@@ -104,7 +104,7 @@ struct TraceParams {
     uint32_t* fold;             // [kFoldWords][rows*width] fold state (ssg_fold_kernel); AUX resume input
     DevCamera cam;
     uint32_t occCap;            // host only: persistent grids hold at most this many workgroups per CU (0 = all)
-    uint32_t prioSlots;         // waves on order positions < prioSlots run at raised issue priority
+    uint32_t prio[3];           // issue priority by order position: < prio[0] -> 3, < prio[1] -> 2, < prio[2] -> 1
     uint32_t slotBase;          // split launches: this launch renders order positions slotBase + [0, numSlots)
     uint32_t gridCUs;           // host only: CUs a persistent grid is sized for (0 = all; split launches)
 };
@@ -1386,9 +1386,12 @@ __global__ void __launch_bounds__(WPB * 64, MINW) trace_kernel(TraceParams P)
     tile = P.order ? P.order[pos] : pos;          // packed coordinates (scatter mode: wave index)
     // Issue priority: the cost order puts the most expensive tiles first, and at full occupancy
     // such a tile's chain runs ~3x slower than alone (tools/occupancy_probe.py) -- long enough to
-    // end the launch.  Waves on the first prioSlots positions take issue slots first (s_setprio),
-    // the others fill the gaps.  Scheduling only: results are identical.
-    if (pos < P.prioSlots) __builtin_amdgcn_s_setprio(3);
+    // end the launch.  Waves on the head of the order take issue slots first (s_setprio), the rest
+    // fill the gaps.  pos is wave-uniform (an SGPR), so only one s_setprio executes.  Scheduling
+    // only: results are identical.
+    if (pos < P.prio[0]) __builtin_amdgcn_s_setprio(3);
+    else if (pos < P.prio[1]) __builtin_amdgcn_s_setprio(2);
+    else if (pos < P.prio[2]) __builtin_amdgcn_s_setprio(1);
     else __builtin_amdgcn_s_setprio(0);
     const PixelCtx pc = pixel_of(P, tile, lane);
     const uint64_t tWave = __builtin_amdgcn_s_memtime();
@@ -1894,7 +1897,8 @@ struct pt_context {
     uint64_t orderSamples = 0;    // samples per pixel of the launch whose tile costs built `order`
     int schedule = 0;             // 0 = cost-sorted tiles (default), 1 = row-major
     uint32_t occupancy = 0;       // tuning knob: workgroups per CU of persistent grids (0 = all that fit)
-    int prioSlots = -1;           // order positions run at raised issue priority (-1 = automatic)
+    int prioMode = 0;             // issue priority: 0 = automatic, 1 = off, 2 = explicit bounds prioBounds
+    uint32_t prioBounds[3] = {0, 0, 0};
     // split launch (pt_set_reserved_cus): the head of the cost order on a reserved set of CUs at low
     // occupancy, the rest on the other CUs, two CU-masked streams running concurrently
     uint32_t resCUs = 0, resWaves = 1, resTiles = 0;
@@ -2560,6 +2564,18 @@ static int run_groups(pt_context* ctx, int variant, const TraceParams& P0, uint3
     return PT_OK;
 }
 
+// Issue priority of a launch over `tiles` order positions (pt_set_issue_priority): position bounds of
+// priority levels 3, 2, 1; the rest run at 0.
+static void issue_priority(const pt_context* ctx, uint32_t tiles, uint32_t* prio)
+{
+    if (ctx->prioMode == 2) {
+        for (int i = 0; i < 3; ++i) prio[i] = ctx->prioBounds[i];
+        return;
+    }
+    for (int i = 0; i < 3; ++i) prio[i] = 0;      // off (automatic policy: set below once measured)
+    (void)tiles;
+}
+
 // Split launch (pt_set_reserved_cus): the first resTiles positions of the cost order
 // -- the most expensive tiles, whose sample chains run ~2-3x slower at full occupancy than alone
 // (tools/occupancy_probe.py) -- render on resCUs CUs at resWaves waves per SIMD (stream masked to
@@ -2713,7 +2729,7 @@ static int render_impl(pt_context* ctx, const pt_camera* cam, uint32_t spp, uint
     P.tileCursor = ctx->tileCursor;
     P.numSlots = tiles;
     P.occCap = ctx->occupancy;
-    P.prioSlots = ctx->prioSlots >= 0 ? (uint32_t)ctx->prioSlots : 0u;
+    issue_priority(ctx, tiles, P.prio);
     if (stats) PT_HIP_CHECK(ctx, hipMemsetAsync(ctx->stats, 0, kStatWords * sizeof(unsigned long long), ctx->stream));
     int variant = pick_variant(ctx);
     // speculative sample groups
@@ -2876,10 +2892,13 @@ PT_API int pt_set_reserved_cus(pt_context* ctx, uint32_t cus, uint32_t waves_per
     return PT_OK;
 }
 
-PT_API int pt_set_priority_slots(pt_context* ctx, int slots)
+PT_API int pt_set_issue_priority(pt_context* ctx, int mode, uint32_t level3, uint32_t level2, uint32_t level1)
 {
-    if (!ctx || slots < -1) return PT_ERR_ARG;
-    ctx->prioSlots = slots;
+    if (!ctx || mode < 0 || mode > 2 || (mode == 2 && !(level3 <= level2 && level2 <= level1))) return PT_ERR_ARG;
+    ctx->prioMode = mode;
+    ctx->prioBounds[0] = level3;
+    ctx->prioBounds[1] = level2;
+    ctx->prioBounds[2] = level1;
     return PT_OK;
 }
 

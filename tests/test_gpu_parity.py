@@ -158,8 +158,9 @@ def test_schedule_knobs_do_not_change_results(gpu_available, scenes):
     pt.render(cam, 4, True, chunks=3)
     want = pt.accum().view(np.uint32).copy()
     want_rng = pt.rng_state()
-    for prio, res, occ in [(64, (0, 1, 0), 0), (0, (16, 1, 0), 0), (256, (32, 2, 300), 0), (0, (0, 1, 0), 2)]:
-        pt.set_priority_slots(prio)
+    for prio, res, occ in [((2, 64, 64, 64), (0, 1, 0), 0), ((1, 0, 0, 0), (16, 1, 0), 0),
+                           ((2, 100, 2000, 6000), (32, 2, 300), 0), ((0, 0, 0, 0), (0, 1, 0), 2)]:
+        pt.set_issue_priority(*prio)
         pt.set_reserved_cus(*res)
         pt.set_occupancy(occ)
         pt.set_rng_state(st)

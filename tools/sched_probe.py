@@ -1,6 +1,9 @@
 """Launch time of one workload under several tile schedules, interleaved rounds in one process,
 results checked bit-identical against the first schedule.  A schedule is a comma-free token:
-    p<K>                 issue priority for the first K positions of the cost order (pt_set_priority_slots)
+    p<K>                 issue priority 3 for the first K positions of the cost order (pt_set_issue_priority)
+    f<F>                 the same for the first F percent of the positions
+    q                    graded: priority 3 / 2 / 1 / 0 by quarter of the order
+    a                    the automatic policy (off: priority 0 for every position)
     r<R>w<W>[k<K>]       split launch: the first K positions (default one per reserved wave slot) on R
                          reserved CUs at W waves per SIMD, the rest on the other CUs (pt_set_reserved_cus)
     r<R>w<W>k<K>p<P>     both
@@ -20,13 +23,22 @@ sys.path.insert(0, str(ROOT))
 import pathtracercuda_amd as pa  # noqa: E402
 
 
-def apply(pt, tok):
-    m = re.fullmatch(r"(?:r(\d+)w(\d+)(?:k(\d+))?)?(?:p(\d+))?", tok)
+def apply(pt, tok, tiles):
+    if tok == "a":
+        pt.set_reserved_cus(0)
+        pt.set_issue_priority(0)
+        return
+    if tok == "q":
+        pt.set_reserved_cus(0)
+        pt.set_issue_priority(2, tiles // 4, tiles // 2, 3 * tiles // 4)
+        return
+    m = re.fullmatch(r"(?:r(\d+)w(\d+)(?:k(\d+))?)?(?:([pf])(\d+))?", tok)
     if not m:
         raise SystemExit(f"bad schedule {tok}")
-    r, w, k, p = m.groups()
+    r, w, k, kind, p = m.groups()
     pt.set_reserved_cus(int(r or 0), int(w or 1), int(k or 0))
-    pt.set_priority_slots(int(p or 0))
+    K = int(p or 0) if kind != "f" else tiles * int(p) // 100
+    pt.set_issue_priority(2, K, K, K)
 
 
 def main():
@@ -53,7 +65,7 @@ def main():
     ref = None
     for r in range(a.rounds):
         for k in (scheds if r % 2 == 0 else scheds[::-1]):
-            apply(pt, k)
+            apply(pt, k, ((a.width + 7) // 8) * ((pt.rows + 7) // 8))
             pt.set_rng_state(st)
             times[k].append(pt.render_raw(cam, 8, a.spp // 8, True))
             cost = pt.tile_costs().ravel().astype(np.float64) / 2.4e6          # ms at 2.4 GHz
