@@ -3,6 +3,7 @@ results checked bit-identical against the first schedule.  A schedule is a comma
     p<K>                 issue priority 3 for the first K positions of the cost order (pt_set_issue_priority)
     f<F>                 the same for the first F percent of the positions
     q                    graded: priority 3 / 2 / 1 / 0 by quarter of the order
+    g<A>_<B>_<C>         graded: priority 3 below A %, 2 below B %, 1 below C % of the positions
     a                    the automatic policy (off: priority 0 for every position)
     r<R>w<W>[k<K>]       split launch: the first K positions (default one per reserved wave slot) on R
                          reserved CUs at W waves per SIMD, the rest on the other CUs (pt_set_reserved_cus)
@@ -31,6 +32,11 @@ def apply(pt, tok, tiles):
     if tok == "q":
         pt.set_reserved_cus(0)
         pt.set_issue_priority(2, tiles // 4, tiles // 2, 3 * tiles // 4)
+        return
+    g = re.fullmatch(r"g(\d+)_(\d+)_(\d+)", tok)
+    if g:                                              # graded, bounds in percent of the positions
+        pt.set_reserved_cus(0)
+        pt.set_issue_priority(2, *(tiles * int(x) // 100 for x in g.groups()))
         return
     m = re.fullmatch(r"(?:r(\d+)w(\d+)(?:k(\d+))?)?(?:([pf])(\d+))?", tok)
     if not m:
