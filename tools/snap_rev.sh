@@ -2,13 +2,15 @@
 # Build libpt_hip.so of an earlier commit into _snap/<name>/ (a minimal tree tools/ab_variants.py
 # runs from) for same-box A/Bs against the working tree (tools/gpu_ab_snap.sh).  Host library and
 # Python package come from the working tree (the C ABI is unchanged between the two).
-#   tools/snap_rev.sh <name> <git-rev> ["<extra hipcc flags>"]
+#   [SED='<sed expression on pt_kernels.hip>'] tools/snap_rev.sh <name> <git-rev> ["<extra hipcc flags>"]
 set -eu
 cd "$(dirname "$0")/.."
 name=$1; rev=$2; flags=${3:-}
 d=_snap/$name; src=$(mktemp -d)
 rm -rf "$d"; mkdir -p "$d/pathtracercuda_amd/lib" "$d/tools"
 git archive "$rev" pathtracercuda_amd/csrc include | tar -x -C "$src"
+# optional source edit for parameter A/Bs, e.g. SED='s/kV40Walk = 13216/kV40Walk = 14216/'
+if [ -n "${SED:-}" ]; then sed -i "$SED" "$src/pathtracercuda_amd/csrc/pt_kernels.hip"; fi
 cp pathtracercuda_amd/*.py "$d/pathtracercuda_amd/"
 cp pathtracercuda_amd/lib/libpt_host.so "$d/pathtracercuda_amd/lib/"
 cp tools/ab_variants.py tools/one_launch.py "$d/tools/"
