@@ -364,6 +364,7 @@ def record(cfg, run, elapsed, kernel_ms, steps, st, n, with_profile=True):
             "frac": None, "traffic": None, "kernel": "trace_kernel", "avg_launch_ms": round(avg_launch_s * 1e3, 3),
             "lds_l2_effective_GBs": round(alg / avg_launch_s / 1e9, 1),
             "bytes_per_sample": round(alg / samples_launch, 1),
+            "segments_per_sample": round(st["segments"] / max(st["samples"], 1), 3),
             "lane_utilisation": lane_utilisation(st)}
     if prof:
         c = prof["counters"]

@@ -205,11 +205,6 @@ PT_API int pt_set_occupancy(pt_context *ctx, uint32_t workgroups_per_cu);
  * rest at 0 (level3 <= level2 <= level1).  Results are identical. */
 PT_API int pt_set_issue_priority(pt_context *ctx, int mode, uint32_t level3, uint32_t level2, uint32_t level1);
 
-/* Split launches (measurement knob, 0 CUs = off, the default): the first `tiles` positions of the
- * cost order (0 = one per reserved wave slot) render on `cus` CUs at `waves_per_simd` waves per SIMD
- * through a CU-masked stream, the rest on the other CUs concurrently.  Results are identical. */
-PT_API int pt_set_reserved_cus(pt_context *ctx, uint32_t cus, uint32_t waves_per_simd, uint32_t tiles);
-
 /* Speculative sample groups.  A pixel's samples are one serial XORWOW stream
  * (trace.cu:183-193), so a launch with fewer 8x8 tiles than about four per wave slot of the chip
  * (multi-GPU strong scaling, small images) lasts as long as its slowest tile's whole chain.  With

@@ -312,12 +312,6 @@ class Pathtracer:
         for c in self._contexts():
             N.check_ctx(N.hip().pt_set_issue_priority(c, int(mode), int(level3), int(level2), int(level1)), c)
 
-    def set_reserved_cus(self, cus: int, waves_per_simd: int = 1, tiles: int = 0) -> None:
-        """Split launches (pt_set_reserved_cus): the head of the cost order on `cus` reserved CUs at
-        low occupancy, the rest on the other CUs; 0 CUs = off.  Results are identical."""
-        for c in self._contexts():
-            N.check_ctx(N.hip().pt_set_reserved_cus(c, int(cus), int(waves_per_simd), int(tiles)), c)
-
     def set_schedule(self, mode: int) -> None:
         """0 = cost-sorted tile dispatch (default), 1 = row-major (pt_set_schedule), every device."""
         for c in self._contexts():

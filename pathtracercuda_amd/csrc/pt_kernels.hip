@@ -105,8 +105,6 @@ struct TraceParams {
     DevCamera cam;
     uint32_t occCap;            // host only: persistent grids hold at most this many workgroups per CU (0 = all)
     uint32_t prio[3];           // issue priority by order position: < prio[0] -> 3, < prio[1] -> 2, < prio[2] -> 1
-    uint32_t slotBase;          // split launches: this launch renders order positions slotBase + [0, numSlots)
-    uint32_t gridCUs;           // host only: CUs a persistent grid is sized for (0 = all; split launches)
 };
 
 // Speculative sample groups: window of a group's start offset in which an earlier group's parse can
@@ -1377,7 +1375,7 @@ __global__ void __launch_bounds__(WPB * 64, MINW) trace_kernel(TraceParams P)
     uint32_t slot = PERSIST ? wave_fetch(P.tileCursor, 1u) : __builtin_amdgcn_readfirstlane(blockIdx.x * (uint32_t)WPB + wave);
     for (;;) {
     if (slot >= P.numSlots) break;               // also the grid's spare slots past the last item
-    uint32_t tile, grp = 0, pos = slot + P.slotBase;  // pos: the tile's position in the order
+    uint32_t tile, grp = 0, pos = slot;              // pos: the tile's position in the order
     if (SSG && !P.ssgPatch) {
         const uint32_t J = 2 * P.ssgG - 1;
         pos = slot / J;
@@ -1899,11 +1897,6 @@ struct pt_context {
     uint32_t occupancy = 0;       // tuning knob: workgroups per CU of persistent grids (0 = all that fit)
     int prioMode = 0;             // issue priority: 0 = automatic, 1 = off, 2 = explicit bounds prioBounds
     uint32_t prioBounds[3] = {0, 0, 0};
-    // split launch (pt_set_reserved_cus): the head of the cost order on a reserved set of CUs at low
-    // occupancy, the rest on the other CUs, two CU-masked streams running concurrently
-    uint32_t resCUs = 0, resWaves = 1, resTiles = 0;
-    hipStream_t resStream = nullptr, mainStream = nullptr;
-    hipEvent_t evFork = nullptr, evRes = nullptr, evMain = nullptr;
     // speculative sample groups
     int ssgMode = 0;              // 0 = automatic, 1 = off, G >= 2 = always G groups (tests)
     uint32_t patchRounds = 6;     // patch rounds before the remaining dead ends run plain
@@ -1998,13 +1991,10 @@ static hipError_t launch_one(const TraceParams& P, hipStream_t stream)
             cap = std::max(cus, 1) * std::max(perCu, 1);
             resident[dev & 63].store(cap);
         }
-        if (P.occCap || P.gridCUs) {                   // fewer waves per SIMD (pt_set_occupancy) or CUs (split)
+        if (P.occCap) {                                // tuning knob (pt_set_occupancy): fewer waves per SIMD
             int cus = 0;
-            if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) == hipSuccess && cus > 0) {
-                const int perCu = cap / cus;
-                if (P.gridCUs) cus = std::min(cus, (int)P.gridCUs);
-                cap = cus * std::min(perCu, P.occCap ? (int)P.occCap : perCu);
-            }
+            if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) == hipSuccess && cus > 0)
+                cap = cus * std::min(cap / cus, (int)P.occCap);
             trace_kernel<STATS, SL, WPB, WW, MINW, PERSIST, MODE><<<(unsigned)cap, WPB * 64, lds, stream>>>(P);
             return hipGetLastError();
         }
@@ -2205,10 +2195,6 @@ PT_API void pt_destroy(pt_context* ctx)
     (void)hipFree(ctx->patchEnd);
     (void)hipFree(ctx->patchCount);
     for (auto& t : ctx->hostTex) (void)hipFree((void*)t.texels);
-    for (hipEvent_t e : {ctx->evFork, ctx->evRes, ctx->evMain})
-        if (e) (void)hipEventDestroy(e);
-    for (hipStream_t q : {ctx->resStream, ctx->mainStream})
-        if (q) (void)hipStreamDestroy(q);
     if (ctx->ev0) (void)hipEventDestroy(ctx->ev0);
     if (ctx->ev1) (void)hipEventDestroy(ctx->ev1);
     if (ctx->stream) (void)hipStreamDestroy(ctx->stream);
@@ -2583,51 +2569,6 @@ static void issue_priority(const pt_context* ctx, uint32_t tiles, uint32_t* prio
     prio[2] = tiles - tiles / 4;
 }
 
-// Split launch (pt_set_reserved_cus): the first resTiles positions of the cost order
-// -- the most expensive tiles, whose sample chains run ~2-3x slower at full occupancy than alone
-// (tools/occupancy_probe.py) -- render on resCUs CUs at resWaves waves per SIMD (stream masked to
-// those CUs), the rest on the other CUs at full occupancy, both concurrently.  Which wave renders a
-// tile changes, never how: results are identical.
-static int launch_split(pt_context* ctx, int variant, const TraceParams& P, uint32_t tiles)
-{
-    int cus = 0;
-    PT_HIP_CHECK(ctx, hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, ctx->device));
-    const uint32_t R = std::min<uint32_t>(ctx->resCUs, (uint32_t)std::max(cus - 8, 0));
-    if (!ctx->resStream) {
-        // reserved CUs spread over the XCDs whether the mask enumerates CUs XCD by XCD or
-        // interleaved: bit k * (cus / R) + (k % 8)
-        std::vector<uint32_t> res((cus + 31) / 32, 0u), rest((cus + 31) / 32, 0u);
-        std::vector<bool> mine(cus, false);
-        for (uint32_t k = 0; k < R; ++k) mine[std::min<uint32_t>(k * (cus / R) + (k % 8), cus - 1)] = true;
-        for (int c = 0; c < cus; ++c) (mine[c] ? res : rest)[c / 32] |= 1u << (c % 32);
-        PT_HIP_CHECK(ctx, hipExtStreamCreateWithCUMask(&ctx->resStream, (uint32_t)res.size(), res.data()));
-        PT_HIP_CHECK(ctx, hipExtStreamCreateWithCUMask(&ctx->mainStream, (uint32_t)rest.size(), rest.data()));
-        PT_HIP_CHECK(ctx, hipEventCreateWithFlags(&ctx->evFork, hipEventDisableTiming));
-        PT_HIP_CHECK(ctx, hipEventCreateWithFlags(&ctx->evRes, hipEventDisableTiming));
-        PT_HIP_CHECK(ctx, hipEventCreateWithFlags(&ctx->evMain, hipEventDisableTiming));
-    }
-    const uint32_t K = std::min<uint32_t>(ctx->resTiles ? ctx->resTiles : R * 4 * ctx->resWaves, tiles);
-    TraceParams A = P, B = P;
-    A.slotBase = 0;
-    A.numSlots = K;
-    A.gridCUs = R;
-    A.occCap = ctx->resWaves;
-    B.slotBase = K;
-    B.numSlots = tiles - K;
-    B.gridCUs = (uint32_t)cus - R;
-    B.tileCursor = ctx->tileCursor + 2;
-    PT_HIP_CHECK(ctx, hipEventRecord(ctx->evFork, ctx->stream));
-    PT_HIP_CHECK(ctx, hipStreamWaitEvent(ctx->resStream, ctx->evFork, 0));
-    PT_HIP_CHECK(ctx, hipStreamWaitEvent(ctx->mainStream, ctx->evFork, 0));
-    if (K) PT_HIP_CHECK(ctx, launch_variant<false>(variant, A, ctx->resStream));
-    if (tiles > K) PT_HIP_CHECK(ctx, launch_variant<false>(variant, B, ctx->mainStream));
-    PT_HIP_CHECK(ctx, hipEventRecord(ctx->evRes, ctx->resStream));
-    PT_HIP_CHECK(ctx, hipEventRecord(ctx->evMain, ctx->mainStream));
-    PT_HIP_CHECK(ctx, hipStreamWaitEvent(ctx->stream, ctx->evRes, 0));
-    PT_HIP_CHECK(ctx, hipStreamWaitEvent(ctx->stream, ctx->evMain, 0));
-    return PT_OK;
-}
-
 static int render_impl(pt_context* ctx, const pt_camera* cam, uint32_t spp, uint32_t chunks, int ignore, float* gpu_ms,
                        pt_render_stats* stats)
 {
@@ -2729,9 +2670,9 @@ static int render_impl(pt_context* ctx, const pt_camera* cam, uint32_t spp, uint
     P.tileCost = sorted ? ctx->tileCost : nullptr;
     P.scatterWaves = ctx->schedule == 2 ? (uint32_t)(((size_t)ctx->rows * ctx->width + 63) / 64) : 0u;
     if (P.scatterWaves) P.order = nullptr;          // scattered mapping: slot = wave index
-    if (!ctx->tileCursor) {                      // two cursor pairs: plain launches and split launches' second half
-        PT_HIP_CHECK(ctx, hipMalloc(&ctx->tileCursor, 4 * sizeof(uint32_t)));
-        PT_HIP_CHECK(ctx, hipMemset(ctx->tileCursor, 0, 4 * sizeof(uint32_t)));
+    if (!ctx->tileCursor) {
+        PT_HIP_CHECK(ctx, hipMalloc(&ctx->tileCursor, 2 * sizeof(uint32_t)));
+        PT_HIP_CHECK(ctx, hipMemset(ctx->tileCursor, 0, 2 * sizeof(uint32_t)));
     }
     P.tileCursor = ctx->tileCursor;
     P.numSlots = tiles;
@@ -2795,9 +2736,6 @@ static int render_impl(pt_context* ctx, const pt_camera* cam, uint32_t spp, uint
         const int rc = run_groups(ctx, variant, P, G, tiles, ssgCap, ctx->stream);
         if (rc != PT_OK) return rc;
         ctx->lastGroups = G;
-    } else if (!stats && ctx->resCUs && P.order && !P.scatterWaves && (variant == 40 || variant == 41 || variant == 46)) {
-        const int rc = launch_split(ctx, variant, P, tiles);
-        if (rc != PT_OK) return rc;
     } else {
         PT_HIP_CHECK(ctx, stats ? launch_variant<true>(variant, P, ctx->stream) : launch_variant<false>(variant, P, ctx->stream));
     }
@@ -2887,15 +2825,6 @@ PT_API int pt_read_group_stats(const pt_context* ctx, uint32_t* dst)
 {
     if (!ctx || !dst) return PT_ERR_ARG;
     memcpy(dst, ctx->groupStats, sizeof(ctx->groupStats));
-    return PT_OK;
-}
-
-PT_API int pt_set_reserved_cus(pt_context* ctx, uint32_t cus, uint32_t waves_per_simd, uint32_t tiles)
-{
-    if (!ctx || cus > 1024 || waves_per_simd < 1 || waves_per_simd > 5) return PT_ERR_ARG;
-    ctx->resCUs = cus;
-    ctx->resWaves = waves_per_simd;
-    ctx->resTiles = tiles;
     return PT_OK;
 }
 

@@ -147,8 +147,8 @@ def test_tile_schedule_does_not_change_results(gpu_available, scenes):
 
 
 def test_schedule_knobs_do_not_change_results(gpu_available, scenes):
-    # issue priority for the head of the cost order, CU-masked split launches (the head on reserved
-    # CUs at low occupancy), occupancy caps: only which wave renders a tile and when changes
+    # issue priority by cost-order position, occupancy caps: only which wave renders a tile and when
+    # changes
     W, H = 1280, 720
     pt = pa.Pathtracer(W, H)
     cam = pt.load_scene(scenes / "generated_scene.scene.json")
@@ -158,15 +158,14 @@ def test_schedule_knobs_do_not_change_results(gpu_available, scenes):
     pt.render(cam, 4, True, chunks=3)
     want = pt.accum().view(np.uint32).copy()
     want_rng = pt.rng_state()
-    for prio, res, occ in [((2, 64, 64, 64), (0, 1, 0), 0), ((1, 0, 0, 0), (16, 1, 0), 0),
-                           ((2, 100, 2000, 6000), (32, 2, 300), 0), ((0, 0, 0, 0), (0, 1, 0), 2)]:
+    for prio, occ in [((2, 64, 64, 64), 0), ((1, 0, 0, 0), 0), ((2, 100, 2000, 6000), 0), ((0, 0, 0, 0), 2),
+                      ((0, 0, 0, 0), 1)]:
         pt.set_issue_priority(*prio)
-        pt.set_reserved_cus(*res)
         pt.set_occupancy(occ)
         pt.set_rng_state(st)
         pt.render(cam, 4, True, chunks=3)
-        assert np.array_equal(pt.accum().view(np.uint32), want), (prio, res, occ)
-        assert np.array_equal(pt.rng_state(), want_rng), (prio, res, occ)
+        assert np.array_equal(pt.accum().view(np.uint32), want), (prio, occ)
+        assert np.array_equal(pt.rng_state(), want_rng), (prio, occ)
 
 
 def test_fast_reciprocal_and_sqrt_exhaustive(gpu_available, root):

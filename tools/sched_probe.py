@@ -4,12 +4,12 @@ results checked bit-identical against the first schedule.  A schedule is a comma
     f<F>                 the same for the first F percent of the positions
     q                    graded: priority 3 / 2 / 1 / 0 by quarter of the order
     g<A>_<B>_<C>         graded: priority 3 below A %, 2 below B %, 1 below C % of the positions
-    a                    the automatic policy (off: priority 0 for every position)
-    r<R>w<W>[k<K>]       split launch: the first K positions (default one per reserved wave slot) on R
-                         reserved CUs at W waves per SIMD, the rest on the other CUs (pt_set_reserved_cus)
-    r<R>w<W>k<K>p<P>     both
+    a                    the automatic policy (graded by quarter since it was measured; "a" meant off before)
+    o                    off: priority 0 for every position
+(The round-3 split-launch tokens r<R>w<W>[k<K>] measured the CU-masked split launches of commit
+2ac067f; the knob was removed after profiles/r03_schedule_sweep.json.)
 Usage on the GPU box:
-    python tools/sched_probe.py [--width 1920 --height 1080 --spp 1024 --n 1] --scheds p0,p256,r16w1,r32w2k256
+    python tools/sched_probe.py [--width 1920 --height 1080 --spp 1024 --n 1] --scheds a,p4096,f25,q
 """
 import argparse
 import json
@@ -25,25 +25,21 @@ import pathtracercuda_amd as pa  # noqa: E402
 
 
 def apply(pt, tok, tiles):
-    if tok == "a":
-        pt.set_reserved_cus(0)
-        pt.set_issue_priority(0)
+    if tok in ("a", "o"):
+        pt.set_issue_priority(0 if tok == "a" else 1)
         return
     if tok == "q":
-        pt.set_reserved_cus(0)
         pt.set_issue_priority(2, tiles // 4, tiles // 2, 3 * tiles // 4)
         return
     g = re.fullmatch(r"g(\d+)_(\d+)_(\d+)", tok)
     if g:                                              # graded, bounds in percent of the positions
-        pt.set_reserved_cus(0)
         pt.set_issue_priority(2, *(tiles * int(x) // 100 for x in g.groups()))
         return
-    m = re.fullmatch(r"(?:r(\d+)w(\d+)(?:k(\d+))?)?(?:([pf])(\d+))?", tok)
+    m = re.fullmatch(r"([pf])(\d+)", tok)
     if not m:
         raise SystemExit(f"bad schedule {tok}")
-    r, w, k, kind, p = m.groups()
-    pt.set_reserved_cus(int(r or 0), int(w or 1), int(k or 0))
-    K = int(p or 0) if kind != "f" else tiles * int(p) // 100
+    kind, p = m.groups()
+    K = int(p) if kind == "p" else tiles * int(p) // 100
     pt.set_issue_priority(2, K, K, K)
 
 
