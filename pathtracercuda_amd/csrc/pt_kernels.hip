@@ -2017,14 +2017,15 @@ static hipError_t launch_one(const TraceParams& P, hipStream_t stream)
 // (deferred shading and the traversal's exit threshold, see trace_kernel).
 //   39  variant 40 without deferred shading, exit <= 24/64 (the round-1 default; A/B reference)
 //   40  default: resumable lean child-box walk, records in LDS, persistent waves, deferred shading
-//       (hits >= 3/8, misses >= 1/8 with a sky texture), exit <= 16/64
+//       (hits >= 4/8, misses >= 1/8 with a sky texture), exit <= 12/64
 //   41  default for cache-read scenes: same, records through the caches, exit <= 12/64
 //   46  default for deep cache-read BVHs: variant 41 compiled for 4 waves/SIMD (128 VGPRs)
 //   47  small grids (<= 4 tiles per SIMD): variant 39 compiled for 4 waves/SIMD (128 VGPRs); no
 //       deferral, which costs a single pass of latency-bound waves 2.8 %
 //   48  small grids whose primitives fit in LDS too: records and primitives in LDS, 4 waves/SIMD,
 //       deferred hits
-constexpr int kV40Walk = 13216;     // variant 40's walk parameters (SKYQ 1, DEFERQ 3, exit <= 16/64)
+constexpr int kV40Walk = 14212;     // variant 40's walk parameters (SKYQ 1, DEFERQ 4, exit <= 12/64;
+                                    // retuned in round 3, profiles/r03_walk_params_ab.json)
 template <bool STATS, int MODE = 0>
 static hipError_t launch_variant(int v, const TraceParams& P, hipStream_t stream)
 {

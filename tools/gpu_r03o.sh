@@ -3,5 +3,5 @@
 # four snapshots with one parameter moved.
 set -u
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
-TAG=r03o/ab SIDES=". _snap/w14216 _snap/w12216 _snap/w13220 _snap/w13212" PAIRS=3 SPP=512 bash tools/gpu_ab_snap.sh || exit 5
+TAG=r03p/ab SIDES=". _snap/w14216 _snap/w15216 _snap/w14212 _snap/w24216 _snap/w4216" PAIRS=3 SPP=512 bash tools/gpu_ab_snap.sh || exit 5
 echo "== done"
