@@ -2018,7 +2018,7 @@ static hipError_t launch_one(const TraceParams& P, hipStream_t stream)
 //   39  variant 40 without deferred shading, exit <= 24/64 (the round-1 default; A/B reference)
 //   40  default: resumable lean child-box walk, records in LDS, persistent waves, deferred shading
 //       (hits >= 4/8, misses >= 1/8 with a sky texture), exit <= 12/64
-//   41  default for cache-read scenes: same, records through the caches, exit <= 12/64
+//   41  default for cache-read scenes: same, records through the caches
 //   46  default for deep cache-read BVHs: variant 41 compiled for 4 waves/SIMD (128 VGPRs)
 //   47  small grids (<= 4 tiles per SIMD): variant 39 compiled for 4 waves/SIMD (128 VGPRs); no
 //       deferral, which costs a single pass of latency-bound waves 2.8 %
@@ -2036,8 +2036,8 @@ static hipError_t launch_variant(int v, const TraceParams& P, hipStream_t stream
     case 20: return launch_one<STATS, 0, 4, 3, 5, false, MODE>(P, stream);
     case 39: return launch_one<STATS, 1, 4, 224, 5, true, MODE>(P, stream);
     case 40: return launch_one<STATS, 1, 4, kV40Walk, 5, true, MODE>(P, stream);
-    case 41: return launch_one<STATS, 0, 4, 13212, 5, true, MODE>(P, stream);
-    case 46: return launch_one<STATS, 0, 4, 13212, 4, true, MODE>(P, stream);
+    case 41: return launch_one<STATS, 0, 4, 14212, 5, true, MODE>(P, stream);
+    case 46: return launch_one<STATS, 0, 4, 14212, 4, true, MODE>(P, stream);
     case 47: return launch_one<STATS, 1, 4, 224, 4, true, MODE>(P, stream);
     case 48: return launch_one<STATS, 2, 4, 13216, 4, true, MODE>(P, stream);
     default: return hipErrorInvalidValue;
@@ -2052,8 +2052,8 @@ static hipError_t launch_grouped(int v, const TraceParams& P, hipStream_t stream
     switch (v) {
     case 39: return launch_one<false, 1, 4, 224, 5, true, MODE>(P, stream);
     case 40: return launch_one<false, 1, 4, kV40Walk, 5, true, MODE>(P, stream);
-    case 41: return launch_one<false, 0, 4, 13212, 5, true, MODE>(P, stream);
-    case 46: return launch_one<false, 0, 4, 13212, 4, true, MODE>(P, stream);
+    case 41: return launch_one<false, 0, 4, 14212, 5, true, MODE>(P, stream);
+    case 46: return launch_one<false, 0, 4, 14212, 4, true, MODE>(P, stream);
     default: return hipErrorInvalidValue;
     }
 }
