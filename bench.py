@@ -322,7 +322,8 @@ def timed(run, steps, warmup, local_rank, dist_on):
 
 
 LANE_KEYS = ("node_tests", "prim_tests", "hits", "sky_lookups", "segments", "wave_node_iters", "wave_prim_iters",
-             "wave_hits", "wave_sky", "leaf_rounds", "family_execs", "family_execs_compacted")
+             "wave_hits", "wave_sky", "leaf_rounds", "family_execs", "family_execs_compacted", "leaf_round_lanes",
+             "leaf_pairs", "family_execs_compacted_in_round")
 
 
 def lane_utilisation(st):
@@ -342,6 +343,12 @@ def lane_utilisation(st):
         out["leaf_family_paths"] = ratio(st["prim_tests"], st["family_execs"])
         out["leaf_family_execs_per_round"] = round(st["family_execs"] / max(st["leaf_rounds"], 1), 3)
         out["leaf_family_execs_per_round_compacted"] = round(st["family_execs_compacted"] / max(st["leaf_rounds"], 1), 3)
+    if st.get("leaf_round_lanes"):
+        # the lanes a leaf round has to work with: compaction can only move pairs onto lanes in the round
+        r = max(st["leaf_rounds"], 1)
+        out["leaf_round_lanes"] = round(st["leaf_round_lanes"] / r, 2)
+        out["leaf_round_pairs"] = round(st["leaf_pairs"] / r, 2)
+        out["leaf_family_execs_per_round_compacted_in_round"] = round(st["family_execs_compacted_in_round"] / r, 3)
     return out
 
 

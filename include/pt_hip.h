@@ -101,6 +101,12 @@ typedef struct pt_render_stats {
     uint64_t leaf_rounds;
     uint64_t family_execs;
     uint64_t family_execs_compacted;
+    /* per leaf round: the lanes taking part and their (lane, primitive) pairs, summed; and the
+     * family-path executions a compaction over only those lanes would need (the pairs in
+     * family-major order, batches of as many pairs as lanes, one execution per batch and family) */
+    uint64_t leaf_round_lanes;
+    uint64_t leaf_pairs;
+    uint64_t family_execs_compacted_in_round;
 } pt_render_stats;
 
 typedef struct pt_context pt_context;

@@ -44,7 +44,8 @@ class PtRenderStats(C.Structure):
                 ("wave_sky", C.c_uint64), ("wave_segments", C.c_uint64), ("cycles_node_walk", C.c_uint64),
                 ("cycles_leaf_tests", C.c_uint64), ("cycles_shading", C.c_uint64), ("cycles_total", C.c_uint64),
                 ("cycles_lane_idle", C.c_uint64), ("leaf_rounds", C.c_uint64), ("family_execs", C.c_uint64),
-                ("family_execs_compacted", C.c_uint64)]
+                ("family_execs_compacted", C.c_uint64), ("leaf_round_lanes", C.c_uint64), ("leaf_pairs", C.c_uint64),
+                ("family_execs_compacted_in_round", C.c_uint64)]
 
 
 # symbol -> (restype, argtypes); the CPU test suite checks that every declaration in include/*.h

@@ -118,7 +118,7 @@ static inline uint32_t ssg_window_words(uint32_t G, uint32_t n)
     return G == 2 ? (n * 6u + 256u + 63u) / 64u : kWinWords;
 }
 constexpr uint32_t kFoldBatch = 16;       // samples the fold loads at once
-constexpr uint32_t kStatWords = 19;       // counters of an instrumented launch (pt_render_stats)
+constexpr uint32_t kStatWords = 22;       // counters of an instrumented launch (pt_render_stats)
 constexpr uint32_t kStartWords = 8;       // start record: offset, d, v0..v4, stop offset (last group)
 enum : uint32_t { F_ACC = 0, F_COL = 3, F_SC = 6, F_DONE = 7, F_OFF = 8, F_H = 9, F_ST = 10, F_FLAG = 16, F_ODD = 17,
                   F_SQ = 18, kFoldWords = 19 };
@@ -227,14 +227,27 @@ PT_DEV bool quadric_roots(uint32_t type, const LocalRay& r, float& t0, float& t1
     return true;
 }
 
-// Hittable::hit without the hit-record side effects: returns the hit distance of prim `p`.
-PT_DEV bool prim_hit(const float4* __restrict__ prims, uint32_t p, f3 o, f3 d, float tMin, float tMax, float& tOut)
+// A primitive's record as the test reads it: the inverse-transform rows and the shape type.
+struct PrimRec {
+    float4 r0, r1, r2;
+    uint32_t type;
+};
+
+PT_DEV PrimRec load_prim(const float4* __restrict__ prims, uint32_t p)
 {
-    const float4 r0 = prims[4 * p + 0];
-    const float4 r1 = prims[4 * p + 1];
-    const float4 r2 = prims[4 * p + 2];
-    const uint32_t type = __float_as_uint(prims[4 * p + 3].x);
-    const LocalRay r = to_local(r0, r1, r2, o, d);
+    PrimRec q;
+    q.r0 = prims[4 * p + 0];
+    q.r1 = prims[4 * p + 1];
+    q.r2 = prims[4 * p + 2];
+    q.type = __float_as_uint(prims[4 * p + 3].x);
+    return q;
+}
+
+// Hittable::hit without the hit-record side effects: returns the hit distance of the primitive.
+PT_DEV bool prim_hit_rec(const PrimRec& q, f3 o, f3 d, float tMin, float tMax, float& tOut)
+{
+    const uint32_t type = q.type;
+    const LocalRay r = to_local(q.r0, q.r1, q.r2, o, d);
     if (type == DISK || type == QUAD) {                    // Hittable.inl:205-235, 299-329
         if (r.d.y == 0.0f) return false;
         const float t = -r.o.y / r.d.y;
@@ -281,6 +294,11 @@ PT_DEV bool prim_hit(const float4* __restrict__ prims, uint32_t p, f3 o, f3 d, f
     return true;
 }
 
+PT_DEV bool prim_hit(const float4* __restrict__ prims, uint32_t p, f3 o, f3 d, float tMin, float tMax, float& tOut)
+{
+    return prim_hit_rec(load_prim(prims, p), o, d, tMin, tMax, tOut);
+}
+
 struct Counters {
     uint32_t node_tests, prim_tests, hits, sky, segments, samples;
     // wave-level executions of the same points (SIMD efficiency = lane count / (64 * wave count))
@@ -289,27 +307,40 @@ struct Counters {
     uint64_t cyc_node, cyc_leaf, cyc_shade, cyc_total;
     uint64_t cyc_lane_idle;     // per lane: cycles between finishing its pixel and the tile's end
     uint32_t w_leaf_rounds, w_fam_exec, w_fam_ideal;   // leaf tests by shape family (pt_render_stats)
+    uint32_t w_leaf_lanes, w_leaf_pairs, w_fam_inplace;  // lanes and (lane, primitive) pairs per leaf round
 };
 
 // Shape family of a primitive test's code path in prim_hit: 0 plane (disk, quad), 1 cube, 2 quadric.
 PT_DEV uint32_t shape_family(uint32_t type) { return (type == DISK || type == QUAD) ? 0u : (type == CUBE ? 1u : 2u); }
 
-// Instrumented variants: one leaf round -- the family-path executions a perfect cross-lane
-// compaction would need (ceil(pairs of the family / 64) per family) -- counted once per wave.
+// Instrumented variants: one leaf round, counted once per wave -- the family-path executions a
+// perfect cross-lane compaction over all 64 lanes would need (ceil(pairs of the family / 64) per
+// family), and the ones a compaction over the lanes that are in the round would need: its pairs in
+// family-major order cut into batches of as many pairs as there are such lanes, one execution per
+// (batch, family) segment.  Also the round's lanes and pairs.
 PT_DEV void leaf_round_stats(const float4* __restrict__ prims, uint32_t off, uint32_t count, Counters& cnt)
 {
     uint32_t nf[3] = {0u, 0u, 0u};
     for (uint32_t k = 0; k < count; ++k) nf[shape_family(__float_as_uint(prims[4 * (off + k) + 3].x))]++;
-    uint32_t ideal = 0;
+    const unsigned long long m = __ballot(1);
+    const uint32_t lanes = (uint32_t)__popcll(m);
+    uint32_t ideal = 0, inplace = 0, start = 0;
 #pragma unroll
     for (int f = 0; f < 3; ++f) {
         uint32_t total = 0;
 #pragma unroll
         for (int b = 0; b < 8; ++b) total += (uint32_t)__popcll(__ballot((nf[f] >> b) & 1u)) << b;
         ideal += (total + 63u) / 64u;
+        if (total) inplace += (start + total - 1u) / lanes - start / lanes + 1u;
+        start += total;
     }
-    const unsigned long long m = __ballot(1);
-    if ((threadIdx.x & 63u) == (uint32_t)(__ffsll((long long)m) - 1)) { cnt.w_leaf_rounds++; cnt.w_fam_ideal += ideal; }
+    if ((threadIdx.x & 63u) == (uint32_t)(__ffsll((long long)m) - 1)) {
+        cnt.w_leaf_rounds++;
+        cnt.w_fam_ideal += ideal;
+        cnt.w_leaf_lanes += lanes;
+        cnt.w_leaf_pairs += start;
+        cnt.w_fam_inplace += inplace;
+    }
 }
 
 // One leaf position: the family paths the wave runs (one per family among its active lanes).
@@ -1080,6 +1111,9 @@ PT_DEV void flush_counters(const TraceParams& P, const Counters& cnt)
     atomicAdd(&P.stats[16], (unsigned long long)cnt.w_leaf_rounds);
     atomicAdd(&P.stats[17], (unsigned long long)cnt.w_fam_exec);
     atomicAdd(&P.stats[18], (unsigned long long)cnt.w_fam_ideal);
+    atomicAdd(&P.stats[19], (unsigned long long)cnt.w_leaf_lanes);
+    atomicAdd(&P.stats[20], (unsigned long long)cnt.w_leaf_pairs);
+    atomicAdd(&P.stats[21], (unsigned long long)cnt.w_fam_inplace);
 }
 
 // One atomic per wave: the first active lane adds n to *cursor; the old value is read back from
@@ -2776,6 +2810,9 @@ static int render_impl(pt_context* ctx, const pt_camera* cam, uint32_t spp, uint
         stats->leaf_rounds = h[16];
         stats->family_execs = h[17];
         stats->family_execs_compacted = h[18];
+        stats->leaf_round_lanes = h[19];
+        stats->leaf_pairs = h[20];
+        stats->family_execs_compacted_in_round = h[21];
     }
     return PT_OK;
 }

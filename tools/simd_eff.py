@@ -1,5 +1,6 @@
 """SIMD efficiency of each phase of the trace kernel (instrumented variant): lane-level events
-divided by 64 x wave-level executions.  Usage: python tools/simd_eff.py [--scene ...] [--variant N]"""
+divided by 64 x wave-level executions, cycle shares of the phases, and the leaf-round counters
+(bench.lane_utilisation).  Usage: python tools/simd_eff.py [--scene ...] [--variants 40,...]"""
 import argparse
 import json
 import pathlib
@@ -8,12 +9,13 @@ import sys
 ROOT = pathlib.Path(__file__).resolve().parents[1]
 sys.path.insert(0, str(ROOT))
 import pathtracercuda_amd as pa  # noqa: E402
+from bench import lane_utilisation  # noqa: E402
 
 ap = argparse.ArgumentParser()
 ap.add_argument("--scene", default=str(ROOT / "scenes/generated_scene.scene.json"))
 ap.add_argument("--width", type=int, default=1920)
 ap.add_argument("--height", type=int, default=1080)
-ap.add_argument("--variants", default="1,3")
+ap.add_argument("--variants", default="40")
 ap.add_argument("--spp", type=int, default=8)
 ap.add_argument("--chunks", type=int, default=1)
 a = ap.parse_args()
@@ -32,5 +34,7 @@ for v in [int(x) for x in a.variants.split(",")]:
     shares = {k: round(st[k] / tot, 3) for k in ("cycles_node_walk", "cycles_leaf_tests", "cycles_shading")}
     res[v] = {"simd_efficiency": eff, "per_sample": per_sample, "cycle_share": shares,
               "wave_cycles_per_sample": round(tot / st["samples"] * 64, 1),
-              "lane_idle_after_pixel_done": round(st["cycles_lane_idle"] / (64.0 * tot), 3)}
-print(json.dumps({"scene": pathlib.Path(a.scene).name, "variants": res}, indent=1))
+              "lane_idle_after_pixel_done": round(st["cycles_lane_idle"] / (64.0 * tot), 3),
+              "lane_utilisation": lane_utilisation(st)}
+print(json.dumps({"scene": pathlib.Path(a.scene).name, "image": f"{a.width}x{a.height}", "spp": a.spp * a.chunks,
+                  "variants": res}, indent=1))
