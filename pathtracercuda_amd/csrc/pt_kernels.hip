@@ -2216,7 +2216,8 @@ struct pt_context {
     uint32_t* tileSpan = nullptr;         // [orderTiles][2]
     // speculative sample groups
     int ssgMode = 0;              // 0 = automatic, 1 = off, G >= 2 = always G groups (tests)
-    int headMode = 0;             // head groups (pt_set_head_groups): 0 = automatic, 1 = off, 2 = explicit
+    int headMode = 0;             // head groups (pt_set_head_groups): 0 = automatic, 1 = off, 2 = explicit head,
+                                  // 3 = explicit tail (the last positions of the order)
     uint32_t headTiles = 0, headG = 0;   // explicit: the first headTiles positions in headG groups
     std::vector<uint32_t> sortedCost;    // the order's tile costs, descending (head-group policy)
     uint32_t patchRounds = 6;     // patch rounds before the remaining dead ends run plain
@@ -2841,7 +2842,8 @@ static int sort_order(pt_context* ctx, uint32_t tiles, uint64_t samples)
 // Guess, grouped launch, fold, patch rounds and resume of speculative sample groups over the first
 // `groupTiles` tiles of P.order (all tiles when P.order is null), on `s`.
 static int run_groups(pt_context* ctx, int variant, const TraceParams& P0, uint32_t G, uint32_t groupTiles,
-                      uint32_t ssgCap, hipStream_t s, const TraceParams* rest = nullptr, hipStream_t restStream = nullptr)
+                      uint32_t ssgCap, hipStream_t s, const TraceParams* rest = nullptr, hipStream_t restStream = nullptr,
+                      bool partial = false)
 {
     TraceParams P = P0;
     const uint32_t total = P.spp * P.chunks;
@@ -2849,7 +2851,7 @@ static int run_groups(pt_context* ctx, int variant, const TraceParams& P0, uint3
     const size_t items = (size_t)groupTiles * (2 * G - 1);
     const unsigned pixBlocks = (unsigned)(((size_t)groupTiles * 64 + 255) / 256);
     P.ssgG = G;
-    P.ssgCostDiv = rest ? 1u : G;
+    P.ssgCostDiv = (rest || partial) ? 1u : G;
     P.ssgTiles = groupTiles;
     P.ssgCap = ssgCap;
     P.ssgLog = ctx->ssgLog;
@@ -2928,11 +2930,11 @@ static void issue_priority(const pt_context* ctx, uint32_t tiles, uint32_t* prio
 static void head_groups(const pt_context* ctx, uint32_t tiles, uint32_t total, uint32_t& K, uint32_t& G)
 {
     K = G = 0;
-    if (ctx->headMode != 2 || ctx->headTiles == 0 || ctx->headG < 2) return;
+    if ((ctx->headMode != 2 && ctx->headMode != 3) || ctx->headTiles == 0 || ctx->headG < 2) return;
     G = std::min<uint32_t>(ctx->headG, std::max(total / 64u, 1u));
     if (G < 2) { G = 0; return; }
     // at most half the tiles and 2,048 grouped items (a quarter of the chip's wave slots)
-    K = std::min<uint32_t>({ctx->headTiles, tiles / 2, 2048u / (2 * G - 1)});
+    K = std::min<uint32_t>({ctx->headTiles, tiles / 2, (ctx->headMode == 3 ? 8192u : 2048u) / (2 * G - 1)});
     if (K == 0) G = 0;
 }
 
@@ -3088,7 +3090,7 @@ static int render_impl(pt_context* ctx, const pt_camera* cam, uint32_t spp, uint
         // state, nothing written back (discard) -- and the launch below already runs in cost order.
         // Progressive 1-spp frames skip it and reuse the previous order for one launch instead.
         TraceParams Q = P;
-        const bool guesses = G != 0 || ctx->headMode == 2;   // speculative groups also take their offset guesses from it
+        const bool guesses = G != 0 || ctx->headMode >= 2;   // speculative groups also take their offset guesses from it
         Q.spp = guesses ? 8u : kPrepassSpp;
         Q.chunks = 1;
         Q.ignoreFirst = 1;
@@ -3142,18 +3144,33 @@ static int render_impl(pt_context* ctx, const pt_camera* cam, uint32_t spp, uint
             PT_HIP_CHECK(ctx, hipMalloc(&ctx->tileCursor2, 2 * sizeof(uint32_t)));
             PT_HIP_CHECK(ctx, hipMemset(ctx->tileCursor2, 0, 2 * sizeof(uint32_t)));
         }
-        // the rest of the order as a plain persistent launch on the second stream, with its own
-        // cursor and its grid short of the workgroups the grouped items occupy
         TraceParams R = P;
-        R.order = P.order + headK;
-        R.numSlots = tiles - headK;
-        R.tileCursor = ctx->tileCursor2;
-        R.gridReserve = (uint32_t)((headK * (2 * (size_t)headG - 1) + 3) / 4);
         R.compTop = 0;
-        issue_priority(ctx, tiles - headK, R.prio);
         PT_HIP_CHECK(ctx, hipEventRecord(ctx->evFork, ctx->stream));
         PT_HIP_CHECK(ctx, hipStreamWaitEvent(ctx->stream2, ctx->evFork, 0));
-        const int rc = run_groups(ctx, variant, P, headG, headK, ssgCap, ctx->stream, &R, ctx->stream2);
+        int rc = PT_OK;
+        if (ctx->headMode == 3) {
+            // tail: the plain launch of the first tiles - K positions goes first and holds every wave
+            // slot; the grouped items of the cheapest tiles (second stream) take the slots its waves
+            // leave when its queue runs dry, so the launch ends on half-length chains
+            R.numSlots = tiles - headK;
+            issue_priority(ctx, tiles - headK, R.prio);
+            PT_HIP_CHECK(ctx, launch_variant<false>(variant, R, ctx->stream));
+            TraceParams Q = P;
+            Q.order = P.order + (tiles - headK);
+            Q.tileCursor = ctx->tileCursor2;
+            for (int i = 0; i < 3; ++i) Q.prio[i] = 0xffffffffu;      // the end of the launch: priority 3
+            rc = run_groups(ctx, variant, Q, headG, headK, ssgCap, ctx->stream2, nullptr, nullptr, true);
+        } else {
+            // head: the rest of the order as a plain persistent launch on the second stream, with its
+            // own cursor and its grid short of the workgroups the grouped items occupy
+            R.order = P.order + headK;
+            R.numSlots = tiles - headK;
+            R.tileCursor = ctx->tileCursor2;
+            R.gridReserve = (uint32_t)((headK * (2 * (size_t)headG - 1) + 3) / 4);
+            issue_priority(ctx, tiles - headK, R.prio);
+            rc = run_groups(ctx, variant, P, headG, headK, ssgCap, ctx->stream, &R, ctx->stream2);
+        }
         if (rc != PT_OK) return rc;
         PT_HIP_CHECK(ctx, hipEventRecord(ctx->evJoin, ctx->stream2));
         PT_HIP_CHECK(ctx, hipStreamWaitEvent(ctx->stream, ctx->evJoin, 0));
@@ -3380,10 +3397,10 @@ PT_API int pt_read_tile_costs(pt_context* ctx, uint32_t* dst, uint32_t count)
 
 PT_API int pt_set_head_groups(pt_context* ctx, int mode, uint32_t tiles, uint32_t groups)
 {
-    if (!ctx || mode < 0 || mode > 2 || (mode == 2 && (groups < 2 || groups > 8))) return PT_ERR_ARG;
+    if (!ctx || mode < 0 || mode > 3 || (mode >= 2 && (groups < 2 || groups > 8))) return PT_ERR_ARG;
     ctx->headMode = mode;
-    ctx->headTiles = mode == 2 ? tiles : 0u;
-    ctx->headG = mode == 2 ? groups : 0u;
+    ctx->headTiles = mode >= 2 ? tiles : 0u;
+    ctx->headG = mode >= 2 ? groups : 0u;
     return PT_OK;
 }
 

@@ -121,6 +121,7 @@ def test_groups_after_plain_launch_reallocate(gpu_available, scenes):
     ("generated_scene", 160, 96, 8, 16, 16, 2, 40),     # 240 tiles: the 16 most expensive in 2 groups
     ("generated_scene", 124, 74, 6, 43, 40, 4, 40),     # ragged, the groups cut render() calls
     ("cornell_box", 96, 64, 5, 40, 24, 3, 41),          # odd spp, records through the caches
+    ("generated_scene", 160, 96, 8, 16, -48, 2, 40),    # tail groups: the 48 cheapest tiles, after the plain launch
 ])
 def test_head_groups_bitexact(gpu_available, scenes, name, W, H, spp, chunks, head, groups, variant):
     """Head groups: the first tiles of the cost order as speculative groups beside a
@@ -135,10 +136,10 @@ def test_head_groups_bitexact(gpu_available, scenes, name, W, H, spp, chunks, he
     st = pt.rng_state()
     pt.render(cam, spp, True, chunks=chunks)          # the cost order
     pt.set_rng_state(st)
-    pt.set_head_groups(2, head, groups)
+    pt.set_head_groups(2 if head > 0 else 3, abs(head), groups)
     pt.render(cam, spp, True, chunks=chunks)
     assert pt.last_sample_groups == groups
-    assert pt.group_log_counts().reshape(-1, 2 * groups - 1, 64)[head:].sum() == 0
+    assert pt.group_log_counts().reshape(-1, 2 * groups - 1, 64)[abs(head):].sum() == 0
     osc = po.load_scene(p, W, H)
     ref = po.OracleRenderer(osc, W, H)
     ref.render(osc.camera, spp, True, chunks=chunks)

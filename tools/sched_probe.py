@@ -25,8 +25,9 @@ import pathtracercuda_amd as pa  # noqa: E402
 
 
 def apply(pt, tok, tiles):
-    h = re.fullmatch(r"h(\d+)g(\d)", tok)               # head groups: the first K positions in G groups
-    pt.set_head_groups(2 if h else 0, int(h.group(1)) if h else 0, int(h.group(2)) if h else 0)
+    h = re.fullmatch(r"([ht])(\d+)g(\d)", tok)          # head (tail) groups: the first (last) K positions in G groups
+    pt.set_head_groups((2 if h.group(1) == "h" else 3) if h else 0, int(h.group(2)) if h else 0,
+                       int(h.group(3)) if h else 0)
     if h:
         pt.set_companion(0)
         pt.set_issue_priority(0)

@@ -11,7 +11,8 @@ rm -rf "$d"; mkdir -p "$d/pathtracercuda_amd/lib" "$d/tools"
 git archive "$rev" pathtracercuda_amd/csrc include | tar -x -C "$src"
 # optional source edit for parameter A/Bs, e.g. SED='s/kV40Walk = 13216/kV40Walk = 14216/'
 if [ -n "${SED:-}" ]; then sed -i "$SED" "$src/pathtracercuda_amd/csrc/pt_kernels.hip"; fi
-cp pathtracercuda_amd/*.py "$d/pathtracercuda_amd/"
+# the Python package of the same revision (it binds exactly that revision's C ABI)
+git archive "$rev" pathtracercuda_amd/__init__.py pathtracercuda_amd/_native.py pathtracercuda_amd/distributed.py | tar -x -C "$d"
 cp pathtracercuda_amd/lib/libpt_host.so "$d/pathtracercuda_amd/lib/"
 cp tools/ab_variants.py tools/one_launch.py "$d/tools/"
 cp -r scenes "$d/"
