@@ -210,18 +210,6 @@ PT_API int pt_set_occupancy(pt_context *ctx, uint32_t workgroups_per_cu);
  * 2 = explicit -- positions < level3 run at wave priority 3, < level2 at 2, < level1 at 1, the
  * rest at 0 (level3 <= level2 <= level1).  Results are identical. */
 PT_API int pt_set_issue_priority(pt_context *ctx, int mode, uint32_t level3, uint32_t level2, uint32_t level1);
-/* Companion scheduling (measurement knob, results identical): order positions < top are "top"
- * tiles; mode 1: a wave whose SIMD runs a top tile takes its next tile from the cheap end of the
- * order; mode 2: it waits until that tile ends (isolation).  mode 0 = off (default). */
-PT_API int pt_set_companion(pt_context *ctx, int mode, uint32_t top);
-/* Head groups: the first `tiles` positions of the cost order run as speculative sample
- * groups of `groups` (2..8) beside a plain launch of the rest (mode 2); mode 1 = off; mode 0 =
- * automatic.  Results are identical. */
-PT_API int pt_set_head_groups(pt_context *ctx, int mode, uint32_t tiles, uint32_t groups);
-/* Tile timeline (diagnostic): record each tile's start and end (s_memrealtime, 100 MHz, low 32 bits)
- * in the next launches; read 2 words per tile (row-major tile index). */
-PT_API int pt_set_tile_spans(pt_context *ctx, int on);
-PT_API int pt_read_tile_spans(pt_context *ctx, uint32_t *dst, uint32_t count);
 
 /* Speculative sample groups.  A pixel's samples are one serial XORWOW stream
  * (trace.cu:183-193), so a launch with fewer 8x8 tiles than about four per wave slot of the chip

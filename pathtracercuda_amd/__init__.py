@@ -312,33 +312,6 @@ class Pathtracer:
         for c in self._contexts():
             N.check_ctx(N.hip().pt_set_issue_priority(c, int(mode), int(level3), int(level2), int(level1)), c)
 
-    def set_companion(self, mode: int, top: int = 0) -> None:
-        """Companion scheduling (pt_set_companion): order positions < top are top tiles; mode 1 =
-        waves sharing a SIMD with a running top tile take the cheap end of the order, 2 = they wait,
-        0 = off.  A measurement knob: results are identical."""
-        for c in self._contexts():
-            N.check_ctx(N.hip().pt_set_companion(c, int(mode), int(top)), c)
-
-    def set_head_groups(self, mode: int, tiles: int = 0, groups: int = 0) -> None:
-        """Head groups (pt_set_head_groups): mode 2 = the first `tiles` positions of the cost order as
-        speculative sample groups of `groups` beside a plain launch of the rest, 1 = off, 0 =
-        automatic.  Results are identical."""
-        for c in self._contexts():
-            N.check_ctx(N.hip().pt_set_head_groups(c, int(mode), int(tiles), int(groups)), c)
-
-    def set_tile_spans(self, on: bool) -> None:
-        """Record each tile's start and end time in the next launches (pt_set_tile_spans)."""
-        for c in self._contexts():
-            N.check_ctx(N.hip().pt_set_tile_spans(c, int(bool(on))), c)
-
-    def tile_spans(self) -> np.ndarray:
-        """(tiles_y, tiles_x, 2) uint32 s_memrealtime ticks (100 MHz) at each tile's start and end."""
-        self._single("tile_spans")
-        tx, ty = (self.width + 7) // 8, (self.rows + 7) // 8
-        out = np.zeros(2 * tx * ty, dtype=np.uint32)
-        N.check_ctx(N.hip().pt_read_tile_spans(self._ctx, out.ctypes.data_as(C.POINTER(C.c_uint32)), tx * ty), self._ctx)
-        return out.reshape(ty, tx, 2)
-
     def set_schedule(self, mode: int) -> None:
         """0 = cost-sorted tile dispatch (default), 1 = row-major (pt_set_schedule), every device."""
         for c in self._contexts():

@@ -95,7 +95,6 @@ struct TraceParams {
     uint32_t ssgTiles;          // grouped tiles: order positions 0 .. ssgTiles - 1
     uint32_t ssgCap;            // sample-log capacity per item
     uint32_t ssgPatch;          // != 0: patch round
-    uint32_t ssgCostDiv;        // an item adds its cycles / ssgCostDiv to its tile's cost
     float* ssgLog;              // [item][cap][3][64] path colours
     uint16_t* ssgEnd;           // [item][cap][64] end of each sample, in draw pairs from the item's start
     const uint32_t* ssgStart;   // [item][8][64] start offset (draw pairs; ~0 = idle lane), d, v0..v4, stop offset
@@ -105,18 +104,8 @@ struct TraceParams {
     uint32_t* fold;             // [kFoldWords][rows*width] fold state (ssg_fold_kernel); AUX resume input
     DevCamera cam;
     uint32_t occCap;            // host only: persistent grids hold at most this many workgroups per CU (0 = all)
-    uint32_t gridReserve;       // host only: persistent grids leave this many resident workgroups free
-                                // (head groups: the grouped items of the top tiles run beside them)
     uint32_t prio[3];           // issue priority by order position: < prio[0] -> 3, < prio[1] -> 2, < prio[2] -> 1
-    // Companion scheduling (pt_set_companion; plain persistent launches): order positions < compTop
-    // are top tiles; a wave whose SIMD runs a top tile takes its next tile from the cheap end of the
-    // order (compMode 1) or waits until the top tile is done (compMode 2, a measurement of isolation).
-    uint32_t compTop, compMode;
-    uint32_t* simdMark;         // [kSimdKeys] top tiles running per SIMD (simd_key)
-    unsigned long long* dualCursor;  // head fetches | tail fetches << 32
-    uint32_t* tileSpan;         // per tile: s_memrealtime (100 MHz, low 32 bits) at start and end (null: off)
 };
-constexpr uint32_t kSimdKeys = 8192;
 
 // Speculative sample groups: window of a group's start offset in which an earlier group's parse can
 // join it (draw pairs; 16 x 64-bit words per lane), and the fold state kept per pixel between rounds.
@@ -1347,44 +1336,6 @@ PT_DEV uint32_t wave_fetch(uint32_t* cursor, uint32_t n)
     return __builtin_amdgcn_readfirstlane(base);
 }
 
-// The SIMD a wave runs on: XCC (3 bits), the CU's shader-engine / array / CU fields of HW_ID
-// (bits 15:8) and the SIMD (bits 5:4) -- a key into simdMark.
-PT_DEV uint32_t simd_key()
-{
-    const uint32_t hw = __builtin_amdgcn_s_getreg((31 << 11) | 4);       // HW_REG_HW_ID, 32 bits
-    const uint32_t xcc = __builtin_amdgcn_s_getreg((3 << 11) | 20);      // HW_REG_XCC_ID, 4 bits
-    return ((xcc & 7u) << 10) | (((hw >> 8) & 0xffu) << 2) | ((hw >> 4) & 3u);
-}
-
-// Companion fetch: one 64-bit cursor counts fetches from the head (most expensive first) and from
-// the tail (cheapest first) of the order; a fetch is valid while head + tail < numSlots, so every
-// slot is taken exactly once.  A wave whose SIMD runs a top tile takes the tail (mode 1) or waits
-// for the top tile to end (mode 2).  Scheduling only: results are identical.
-PT_DEV uint32_t companion_fetch(const TraceParams& P, uint32_t key)
-{
-    const unsigned long long m = __ballot(1);
-    const uint32_t leader = (uint32_t)(__ffsll((long long)m) - 1);
-    uint32_t slot = 0;
-    if ((threadIdx.x & 63u) == leader) {
-        for (;;) {
-            const uint32_t mark = __hip_atomic_load(&P.simdMark[key], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            if (mark != 0u && P.compMode == 2u) {
-                const unsigned long long c = __hip_atomic_load(P.dualCursor, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                if ((uint32_t)c + (uint32_t)(c >> 32) < P.numSlots) {
-                    __builtin_amdgcn_s_sleep(64);
-                    continue;
-                }
-            }
-            const bool tail = mark != 0u && P.compMode == 1u;
-            const unsigned long long old = atomicAdd(P.dualCursor, tail ? (1ull << 32) : 1ull);
-            const uint32_t h = (uint32_t)old, t = (uint32_t)(old >> 32);
-            slot = h + t >= P.numSlots ? P.numSlots : (tail ? P.numSlots - 1u - t : h);
-            break;
-        }
-    }
-    return __builtin_amdgcn_readfirstlane(slot);
-}
-
 // ---------------------------------------------------------------------------------------------
 // Speculative sample groups.  A pixel's samples are one serial XORWOW stream, so
 // a tile costs as long as its slowest pixel's whole chain.  When a launch holds too few tiles to
@@ -1668,10 +1619,7 @@ __global__ void __launch_bounds__(WPB * 64, MINW) trace_kernel(TraceParams P)
                                  wave * kCompactScratch
                            : nullptr;
     Counters cnt = {};
-    const bool comp = PERSIST && MODE == 0 && P.compTop != 0u;
-    const uint32_t skey = comp ? simd_key() : 0u;
-    uint32_t slot = PERSIST ? (comp ? companion_fetch(P, skey) : wave_fetch(P.tileCursor, 1u))
-                            : __builtin_amdgcn_readfirstlane(blockIdx.x * (uint32_t)WPB + wave);
+    uint32_t slot = PERSIST ? wave_fetch(P.tileCursor, 1u) : __builtin_amdgcn_readfirstlane(blockIdx.x * (uint32_t)WPB + wave);
     for (;;) {
     if (slot >= P.numSlots) break;               // also the grid's spare slots past the last item
     uint32_t tile, grp = 0, pos = slot;              // pos: the tile's position in the order
@@ -1690,11 +1638,8 @@ __global__ void __launch_bounds__(WPB * 64, MINW) trace_kernel(TraceParams P)
     else if (pos < P.prio[1]) __builtin_amdgcn_s_setprio(2);
     else if (pos < P.prio[2]) __builtin_amdgcn_s_setprio(1);
     else __builtin_amdgcn_s_setprio(0);
-    const bool top = comp && pos < P.compTop;
-    if (top && lane == 0) atomicAdd(&P.simdMark[skey], 1u);
     const PixelCtx pc = pixel_of(P, tile, lane);
     const uint64_t tWave = __builtin_amdgcn_s_memtime();
-    const uint32_t tReal = P.tileSpan ? (uint32_t)__builtin_amdgcn_s_memrealtime() : 0u;
     const bool run = pc.valid && (!AUX || !P.fold || (P.fold[F_FLAG * pc.npix + pc.li] & 1u));
     if (run) {
         Xorwow rng;
@@ -1772,18 +1717,11 @@ __global__ void __launch_bounds__(WPB * 64, MINW) trace_kernel(TraceParams P)
     if (P.tileCost && lane == 0 && (tile >> 16) < P.tilesY) {
         const uint32_t cyc = (uint32_t)min(__builtin_amdgcn_s_memtime() - tWave, (uint64_t)0xffffffffu);
         const uint32_t lin = (tile >> 16) * P.tilesX + (tile & 0xffffu);
-        // zeroed before the launch (idle items add ~0); a whole grouped launch records chain / G per
-        // tile, head groups (ssgCostDiv 1) the tile's whole chain so that it keeps its place in the order
-        if (SSG) atomicAdd(&P.tileCost[lin], cyc / P.ssgCostDiv);
+        if (SSG) atomicAdd(&P.tileCost[lin], cyc / P.ssgG);   // zeroed before the launch (idle items add ~0)
         else P.tileCost[lin] = cyc;
-        if (P.tileSpan && !SSG) {
-            P.tileSpan[2 * lin] = tReal;
-            P.tileSpan[2 * lin + 1] = (uint32_t)__builtin_amdgcn_s_memrealtime();
-        }
     }
-    if (top && lane == 0) atomicSub(&P.simdMark[skey], 1u);
     if (!PERSIST) break;
-    slot = comp ? companion_fetch(P, skey) : wave_fetch(P.tileCursor, 1u);
+    slot = wave_fetch(P.tileCursor, 1u);
     }
     if (PERSIST) {
         // the last wave to leave rewinds the cursor for the next launch (every wave has made its
@@ -1791,7 +1729,6 @@ __global__ void __launch_bounds__(WPB * 64, MINW) trace_kernel(TraceParams P)
         if (wave_fetch(P.tileCursor + 1, 1u) == gridDim.x * (uint32_t)WPB - 1 && lane == 0) {
             P.tileCursor[0] = 0;
             P.tileCursor[1] = 0;
-            if (comp) *P.dualCursor = 0ull;
         }
     }
     flush_counters<STATS>(P, cnt);
@@ -2173,9 +2110,6 @@ struct pt_context {
     int device = 0;
     hipStream_t stream = nullptr;
     hipEvent_t ev0 = nullptr, ev1 = nullptr;
-    hipStream_t stream2 = nullptr;            // head groups: the plain remainder of the launch
-    hipEvent_t evFork = nullptr, evJoin = nullptr;
-    uint32_t* tileCursor2 = nullptr;          // its own persistent cursor
     uint32_t width = 0, height = 0, rowOffset = 0, rowStride = 1, rows = 0, bandShift = 0;
     float4* accum = nullptr;
     uint32_t* rng = nullptr;
@@ -2210,16 +2144,8 @@ struct pt_context {
     uint32_t occupancy = 0;       // tuning knob: workgroups per CU of persistent grids (0 = all that fit)
     int prioMode = 0;             // issue priority: 0 = automatic, 1 = off, 2 = explicit bounds prioBounds
     uint32_t prioBounds[3] = {0, 0, 0};
-    uint32_t compMode = 0, compTop = 0;   // companion scheduling (pt_set_companion; 0 = off)
-    uint32_t* simdMark = nullptr;         // [kSimdKeys] + the 64-bit dual cursor
-    bool recordSpans = false;             // pt_set_tile_spans
-    uint32_t* tileSpan = nullptr;         // [orderTiles][2]
     // speculative sample groups
     int ssgMode = 0;              // 0 = automatic, 1 = off, G >= 2 = always G groups (tests)
-    int headMode = 0;             // head groups (pt_set_head_groups): 0 = automatic, 1 = off, 2 = explicit head,
-                                  // 3 = explicit tail (the last positions of the order)
-    uint32_t headTiles = 0, headG = 0;   // explicit: the first headTiles positions in headG groups
-    std::vector<uint32_t> sortedCost;    // the order's tile costs, descending (head-group policy)
     uint32_t patchRounds = 6;     // patch rounds before the remaining dead ends run plain
     float* pairs = nullptr;       // per-pixel draw pairs per sample (start-offset guesses)
     bool pairsValid = false;
@@ -2236,7 +2162,6 @@ struct pt_context {
     size_t ssgItems = 0, ssgSamples = 0, patchSamples = 0;   // allocated capacities (records)
     size_t ssgBitsWords = 0;
     uint32_t lastGroups = 0;      // groups of the last launch (0 = plain launch)
-    uint32_t lastGroupTiles = 0;  // order positions the groups covered (all tiles, or the head)
     uint32_t groupStats[10] = {}; // G, patch rounds, dead-end pixels after fold rounds 0..7
     pt_camera lastCam = {};
     uint64_t epoch = 0;           // launches that wrote the accumulation (a group's gather cache key)
@@ -2321,7 +2246,6 @@ static hipError_t launch_one(const TraceParams& P, hipStream_t stream)
             trace_kernel<STATS, SL, WPB, WW, MINW, PERSIST, MODE><<<(unsigned)cap, WPB * 64, lds, stream>>>(P);
             return hipGetLastError();
         }
-        if (P.gridReserve) cap = std::max(cap - (int)P.gridReserve, 1);
         if (blocks <= (unsigned)cap) return launch_one<STATS, SL, WPB, WW, MINW, false, MODE>(P, stream);
         blocks = (unsigned)cap;
     }
@@ -2507,8 +2431,6 @@ PT_API void pt_destroy(pt_context* ctx)
     (void)hipFree(ctx->order);
     (void)hipFree(ctx->rowMajor);
     (void)hipFree(ctx->tileCursor);
-    (void)hipFree(ctx->simdMark);
-    (void)hipFree(ctx->tileSpan);
     (void)hipFree(ctx->ldr);
     (void)hipFree(ctx->sortKeys);
     (void)hipFree(ctx->tileIds);
@@ -2527,10 +2449,6 @@ PT_API void pt_destroy(pt_context* ctx)
     (void)hipFree(ctx->patchEnd);
     (void)hipFree(ctx->patchCount);
     for (auto& t : ctx->hostTex) (void)hipFree((void*)t.texels);
-    if (ctx->evFork) (void)hipEventDestroy(ctx->evFork);
-    if (ctx->evJoin) (void)hipEventDestroy(ctx->evJoin);
-    if (ctx->stream2) (void)hipStreamDestroy(ctx->stream2);
-    (void)hipFree(ctx->tileCursor2);
     if (ctx->ev0) (void)hipEventDestroy(ctx->ev0);
     if (ctx->ev1) (void)hipEventDestroy(ctx->ev1);
     if (ctx->stream) (void)hipStreamDestroy(ctx->stream);
@@ -2830,9 +2748,6 @@ static int sort_order(pt_context* ctx, uint32_t tiles, uint64_t samples)
     size_t bytes = ctx->sortTempBytes;
     PT_HIP_CHECK(ctx, rocprim::radix_sort_pairs_desc(ctx->sortTemp, bytes, ctx->tileCost, ctx->sortKeys, ctx->tileIds,
                                                      ctx->order, tiles, 0, 32, ctx->stream));
-    ctx->sortedCost.resize(tiles);
-    PT_HIP_CHECK(ctx, hipMemcpyAsync(ctx->sortedCost.data(), ctx->sortKeys, (size_t)tiles * sizeof(uint32_t),
-                                     hipMemcpyDeviceToHost, ctx->stream));
     PT_HIP_CHECK(ctx, hipStreamSynchronize(ctx->stream));
     ctx->orderValid = true;
     ctx->orderStale = false;
@@ -2842,8 +2757,7 @@ static int sort_order(pt_context* ctx, uint32_t tiles, uint64_t samples)
 // Guess, grouped launch, fold, patch rounds and resume of speculative sample groups over the first
 // `groupTiles` tiles of P.order (all tiles when P.order is null), on `s`.
 static int run_groups(pt_context* ctx, int variant, const TraceParams& P0, uint32_t G, uint32_t groupTiles,
-                      uint32_t ssgCap, hipStream_t s, const TraceParams* rest = nullptr, hipStream_t restStream = nullptr,
-                      bool partial = false)
+                      uint32_t ssgCap, hipStream_t s)
 {
     TraceParams P = P0;
     const uint32_t total = P.spp * P.chunks;
@@ -2851,7 +2765,6 @@ static int run_groups(pt_context* ctx, int variant, const TraceParams& P0, uint3
     const size_t items = (size_t)groupTiles * (2 * G - 1);
     const unsigned pixBlocks = (unsigned)(((size_t)groupTiles * 64 + 255) / 256);
     P.ssgG = G;
-    P.ssgCostDiv = (rest || partial) ? 1u : G;
     P.ssgTiles = groupTiles;
     P.ssgCap = ssgCap;
     P.ssgLog = ctx->ssgLog;
@@ -2868,9 +2781,6 @@ static int run_groups(pt_context* ctx, int variant, const TraceParams& P0, uint3
     ssg_guess_kernel<<<pixBlocks, 256, 0, s>>>(P, ctx->pairs, ssgN, ctx->ssgStart);
     PT_HIP_CHECK(ctx, hipGetLastError());
     PT_HIP_CHECK(ctx, launch_grouped<1>(variant, P, s));
-    // head groups: the plain remainder goes in after the grouped items (which take their wave
-    // slots first; the remainder's persistent grid leaves them free, gridReserve)
-    if (rest) PT_HIP_CHECK(ctx, launch_variant<false>(variant, *rest, restStream));
     ssg_fold_kernel<<<pixBlocks, 256, 0, s>>>(P, 0, ctx->patchLog, ctx->patchEnd, ctx->patchCount, ssgCap, ctx->pairs,
                                               ctx->deadCount);
     PT_HIP_CHECK(ctx, hipGetLastError());
@@ -2924,18 +2834,6 @@ static void issue_priority(const pt_context* ctx, uint32_t tiles, uint32_t* prio
     prio[0] = tiles / 4;
     prio[1] = tiles / 2;
     prio[2] = tiles - tiles / 4;
-}
-
-// Head groups of a launch: the first K positions of the cost order in G groups (0 = none).
-static void head_groups(const pt_context* ctx, uint32_t tiles, uint32_t total, uint32_t& K, uint32_t& G)
-{
-    K = G = 0;
-    if ((ctx->headMode != 2 && ctx->headMode != 3) || ctx->headTiles == 0 || ctx->headG < 2) return;
-    G = std::min<uint32_t>(ctx->headG, std::max(total / 64u, 1u));
-    if (G < 2) { G = 0; return; }
-    // at most half the tiles and 2,048 grouped items (a quarter of the chip's wave slots)
-    K = std::min<uint32_t>({ctx->headTiles, tiles / 2, (ctx->headMode == 3 ? 8192u : 2048u) / (2 * G - 1)});
-    if (K == 0) G = 0;
 }
 
 static int render_impl(pt_context* ctx, const pt_camera* cam, uint32_t spp, uint32_t chunks, int ignore, float* gpu_ms,
@@ -3047,21 +2945,6 @@ static int render_impl(pt_context* ctx, const pt_camera* cam, uint32_t spp, uint
     P.numSlots = tiles;
     P.occCap = ctx->occupancy;
     issue_priority(ctx, tiles, P.prio);
-    if (ctx->compMode && sorted && !P.scatterWaves) {
-        if (!ctx->simdMark) {
-            PT_HIP_CHECK(ctx, hipMalloc(&ctx->simdMark, kSimdKeys * sizeof(uint32_t) + sizeof(unsigned long long)));
-            PT_HIP_CHECK(ctx, hipMemset(ctx->simdMark, 0, kSimdKeys * sizeof(uint32_t) + sizeof(unsigned long long)));
-        }
-        P.compMode = ctx->compMode;
-        P.compTop = std::min(ctx->compTop, tiles);
-        P.simdMark = ctx->simdMark;
-        P.dualCursor = reinterpret_cast<unsigned long long*>(ctx->simdMark + kSimdKeys);
-    }
-    if (ctx->recordSpans && sorted) {
-        if (ctx->tileSpan && ctx->orderTiles != tiles) { (void)hipFree(ctx->tileSpan); ctx->tileSpan = nullptr; }
-        if (!ctx->tileSpan) PT_HIP_CHECK(ctx, hipMalloc(&ctx->tileSpan, 2 * (size_t)tiles * sizeof(uint32_t)));
-        P.tileSpan = ctx->tileSpan;
-    }
     if (stats) PT_HIP_CHECK(ctx, hipMemsetAsync(ctx->stats, 0, kStatWords * sizeof(unsigned long long), ctx->stream));
     int variant = pick_variant(ctx);
     // speculative sample groups
@@ -3090,7 +2973,7 @@ static int render_impl(pt_context* ctx, const pt_camera* cam, uint32_t spp, uint
         // state, nothing written back (discard) -- and the launch below already runs in cost order.
         // Progressive 1-spp frames skip it and reuse the previous order for one launch instead.
         TraceParams Q = P;
-        const bool guesses = G != 0 || ctx->headMode >= 2;   // speculative groups also take their offset guesses from it
+        const bool guesses = G != 0;           // speculative groups also take their offset guesses from it
         Q.spp = guesses ? 8u : kPrepassSpp;
         Q.chunks = 1;
         Q.ignoreFirst = 1;
@@ -3103,22 +2986,7 @@ static int render_impl(pt_context* ctx, const pt_camera* cam, uint32_t spp, uint
         if (rs != PT_OK) return rs;
         P.order = ctx->order;
     }
-    // Head groups: only the most expensive tiles of the order run as speculative
-    // sample groups -- their chains, not the chip's throughput, set the length of a launch with few
-    // tiles per wave slot -- beside a plain launch of the rest.
-    uint32_t headK = 0, headG = 0;
-    if (!G && groupable && P.order == ctx->order && ctx->orderValid &&
-        (variant == 39 || variant == 40 || variant == 41 || variant == 46))
-        head_groups(ctx, tiles, total, headK, headG);
     uint32_t ssgCap = 0;
-    if (headK) {
-        const uint32_t ssgN = total / headG;
-        ssgCap = std::min<uint32_t>({total, 2 * ssgN + 64, 10000u});
-        const size_t J = 2 * (size_t)headG - 1;
-        if (!ssg_reserve(ctx, tiles, (size_t)headK * J, (size_t)headK * J * ssgCap, (size_t)headK * ssgCap,
-                         (size_t)headK * J * ssg_window_words(headG, ssgN)))
-            headK = 0;
-    }
     if (G) {
         const uint32_t ssgN = total / G;
         // an item runs its group and, where the next group's guess missed, into the group after it;
@@ -3129,53 +2997,12 @@ static int render_impl(pt_context* ctx, const pt_camera* cam, uint32_t spp, uint
                          (size_t)tiles * J * ssg_window_words(G, ssgN)))
             G = 0;
     }
-    if (!G && !headK) ssg_release(ctx);
-    if ((G || headK) && P.tileCost) PT_HIP_CHECK(ctx, hipMemsetAsync(P.tileCost, 0, (size_t)tiles * sizeof(uint32_t), ctx->stream));
+    if (!G) ssg_release(ctx);
+    if (G && P.tileCost) PT_HIP_CHECK(ctx, hipMemsetAsync(P.tileCost, 0, (size_t)tiles * sizeof(uint32_t), ctx->stream));
     if (G) {
         const int rc = run_groups(ctx, variant, P, G, tiles, ssgCap, ctx->stream);
         if (rc != PT_OK) return rc;
         ctx->lastGroups = G;
-        ctx->lastGroupTiles = tiles;
-    } else if (headK) {
-        if (!ctx->stream2) {
-            PT_HIP_CHECK(ctx, hipStreamCreateWithFlags(&ctx->stream2, hipStreamNonBlocking));
-            PT_HIP_CHECK(ctx, hipEventCreateWithFlags(&ctx->evFork, hipEventDisableTiming));
-            PT_HIP_CHECK(ctx, hipEventCreateWithFlags(&ctx->evJoin, hipEventDisableTiming));
-            PT_HIP_CHECK(ctx, hipMalloc(&ctx->tileCursor2, 2 * sizeof(uint32_t)));
-            PT_HIP_CHECK(ctx, hipMemset(ctx->tileCursor2, 0, 2 * sizeof(uint32_t)));
-        }
-        TraceParams R = P;
-        R.compTop = 0;
-        PT_HIP_CHECK(ctx, hipEventRecord(ctx->evFork, ctx->stream));
-        PT_HIP_CHECK(ctx, hipStreamWaitEvent(ctx->stream2, ctx->evFork, 0));
-        int rc = PT_OK;
-        if (ctx->headMode == 3) {
-            // tail: the plain launch of the first tiles - K positions goes first and holds every wave
-            // slot; the grouped items of the cheapest tiles (second stream) take the slots its waves
-            // leave when its queue runs dry, so the launch ends on half-length chains
-            R.numSlots = tiles - headK;
-            issue_priority(ctx, tiles - headK, R.prio);
-            PT_HIP_CHECK(ctx, launch_variant<false>(variant, R, ctx->stream));
-            TraceParams Q = P;
-            Q.order = P.order + (tiles - headK);
-            Q.tileCursor = ctx->tileCursor2;
-            for (int i = 0; i < 3; ++i) Q.prio[i] = 0xffffffffu;      // the end of the launch: priority 3
-            rc = run_groups(ctx, variant, Q, headG, headK, ssgCap, ctx->stream2, nullptr, nullptr, true);
-        } else {
-            // head: the rest of the order as a plain persistent launch on the second stream, with its
-            // own cursor and its grid short of the workgroups the grouped items occupy
-            R.order = P.order + headK;
-            R.numSlots = tiles - headK;
-            R.tileCursor = ctx->tileCursor2;
-            R.gridReserve = (uint32_t)((headK * (2 * (size_t)headG - 1) + 3) / 4);
-            issue_priority(ctx, tiles - headK, R.prio);
-            rc = run_groups(ctx, variant, P, headG, headK, ssgCap, ctx->stream, &R, ctx->stream2);
-        }
-        if (rc != PT_OK) return rc;
-        PT_HIP_CHECK(ctx, hipEventRecord(ctx->evJoin, ctx->stream2));
-        PT_HIP_CHECK(ctx, hipStreamWaitEvent(ctx->stream, ctx->evJoin, 0));
-        ctx->lastGroups = headG;
-        ctx->lastGroupTiles = headK;
     } else {
         PT_HIP_CHECK(ctx, stats ? launch_variant<true>(variant, P, ctx->stream) : launch_variant<false>(variant, P, ctx->stream));
     }
@@ -3246,7 +3073,7 @@ PT_API int pt_read_group_log_counts(pt_context* ctx, uint32_t* dst, size_t count
 {
     if (!ctx || !dst) return PT_ERR_ARG;
     if (!ctx->ssgCount || ctx->lastGroups == 0) return PT_ERR_STATE;
-    const size_t n = (size_t)ctx->lastGroupTiles * (2 * ctx->lastGroups - 1) * 64;
+    const size_t n = (size_t)((ctx->width + 7) / 8) * ((ctx->rows + 7) / 8) * (2 * ctx->lastGroups - 1) * 64;
     if (count < n) return PT_ERR_ARG;
     PT_HIP_CHECK(ctx, hipSetDevice(ctx->device));
     PT_HIP_CHECK(ctx, hipMemcpy(dst, ctx->ssgCount, n * sizeof(uint32_t), hipMemcpyDeviceToHost));
@@ -3392,41 +3219,6 @@ PT_API int pt_read_tile_costs(pt_context* ctx, uint32_t* dst, uint32_t count)
     PT_HIP_CHECK(ctx, hipSetDevice(ctx->device));
     PT_HIP_CHECK(ctx, hipStreamSynchronize(ctx->stream));
     PT_HIP_CHECK(ctx, hipMemcpy(dst, ctx->tileCost, (size_t)count * sizeof(uint32_t), hipMemcpyDeviceToHost));
-    return PT_OK;
-}
-
-PT_API int pt_set_head_groups(pt_context* ctx, int mode, uint32_t tiles, uint32_t groups)
-{
-    if (!ctx || mode < 0 || mode > 3 || (mode >= 2 && (groups < 2 || groups > 8))) return PT_ERR_ARG;
-    ctx->headMode = mode;
-    ctx->headTiles = mode >= 2 ? tiles : 0u;
-    ctx->headG = mode >= 2 ? groups : 0u;
-    return PT_OK;
-}
-
-PT_API int pt_set_companion(pt_context* ctx, int mode, uint32_t top)
-{
-    if (!ctx || mode < 0 || mode > 2) return PT_ERR_ARG;
-    ctx->compMode = mode ? (uint32_t)mode : 0u;
-    ctx->compTop = mode ? top : 0u;
-    if (mode && top == 0) ctx->compMode = 0;
-    return PT_OK;
-}
-
-PT_API int pt_set_tile_spans(pt_context* ctx, int on)
-{
-    if (!ctx) return PT_ERR_ARG;
-    ctx->recordSpans = on != 0;
-    return PT_OK;
-}
-
-PT_API int pt_read_tile_spans(pt_context* ctx, uint32_t* dst, uint32_t count)
-{
-    if (!ctx || !dst) return PT_ERR_ARG;
-    if (!ctx->tileSpan || count != ctx->orderTiles) return fail(ctx, PT_ERR_STATE, "pt_read_tile_spans: no spans of that size");
-    PT_HIP_CHECK(ctx, hipSetDevice(ctx->device));
-    PT_HIP_CHECK(ctx, hipStreamSynchronize(ctx->stream));
-    PT_HIP_CHECK(ctx, hipMemcpy(dst, ctx->tileSpan, 2 * (size_t)count * sizeof(uint32_t), hipMemcpyDeviceToHost));
     return PT_OK;
 }
 

@@ -186,22 +186,6 @@ def test_schedule_knobs_do_not_change_results(gpu_available, scenes):
         pt.render(cam, 4, True, chunks=3)
         assert np.array_equal(pt.accum().view(np.uint32), want), (prio, occ)
         assert np.array_equal(pt.rng_state(), want_rng), (prio, occ)
-    pt.set_issue_priority(0)
-    pt.set_occupancy(0)
-    # companion scheduling (cheap tiles from the order's tail beside a top tile, or waiting), with the
-    # tile timeline recorded; every tile is rendered exactly once
-    pt.set_tile_spans(True)
-    for mode, top in [(1, 64), (1, 100000), (2, 16)]:
-        pt.set_companion(mode, top)
-        for _ in range(2):                            # the dual cursor is rewound by the last wave
-            pt.set_rng_state(st)
-            pt.render(cam, 4, True, chunks=3)
-            assert np.array_equal(pt.accum().view(np.uint32), want), (mode, top)
-            assert np.array_equal(pt.rng_state(), want_rng), (mode, top)
-        sp = pt.tile_spans().reshape(-1, 2).astype(np.int64)
-        assert ((sp[:, 1] - sp[:, 0]) % (1 << 32) < 10 ** 9).all()
-    pt.set_companion(0)
-    pt.set_tile_spans(False)
 
 
 def test_fast_reciprocal_and_sqrt_exhaustive(gpu_available, root):

@@ -115,42 +115,3 @@ def test_groups_after_plain_launch_reallocate(gpu_available, scenes):
         b.render(cam, 8, ignore, chunks=16)
         same(a.accum(), b.accum(), f"groups {mode}")
         assert np.array_equal(a.rng_state(), b.rng_state())
-
-
-@pytest.mark.parametrize("name,W,H,spp,chunks,head,groups,variant", [
-    ("generated_scene", 160, 96, 8, 16, 16, 2, 40),     # 240 tiles: the 16 most expensive in 2 groups
-    ("generated_scene", 124, 74, 6, 43, 40, 4, 40),     # ragged, the groups cut render() calls
-    ("cornell_box", 96, 64, 5, 40, 24, 3, 41),          # odd spp, records through the caches
-    ("generated_scene", 160, 96, 8, 16, -48, 2, 40),    # tail groups: the 48 cheapest tiles, after the plain launch
-])
-def test_head_groups_bitexact(gpu_available, scenes, name, W, H, spp, chunks, head, groups, variant):
-    """Head groups: the first tiles of the cost order as speculative groups beside a
-    plain persistent launch of the rest on a second stream: the oracle's sums and states, over two
-    launches (history carried), and the plain launch of the same context.  (Groups are at least 64
-    samples long: spp x chunks >= 64 G.)"""
-    p = scenes / f"{name}.scene.json"
-    pt = pa.Pathtracer(W, H)
-    cam = pt.load_scene(str(p))
-    pt.set_kernel_variant(variant)
-    pt.set_sample_groups(1)                           # no whole-launch groups (small images get them)
-    st = pt.rng_state()
-    pt.render(cam, spp, True, chunks=chunks)          # the cost order
-    pt.set_rng_state(st)
-    pt.set_head_groups(2 if head > 0 else 3, abs(head), groups)
-    pt.render(cam, spp, True, chunks=chunks)
-    assert pt.last_sample_groups == groups
-    assert pt.group_log_counts().reshape(-1, 2 * groups - 1, 64)[abs(head):].sum() == 0
-    osc = po.load_scene(p, W, H)
-    ref = po.OracleRenderer(osc, W, H)
-    ref.render(osc.camera, spp, True, chunks=chunks)
-    same(pt.accum(), ref.accum, f"{name} head {head} G={groups}")
-    assert np.array_equal(pt.rng_state(), ref.rng_array())
-    pt.render(cam, spp, False, chunks=chunks)
-    ref.render(osc.camera, spp, False, chunks=chunks)
-    same(pt.accum(), ref.accum, f"{name} head {head} G={groups}, second launch")
-    assert np.array_equal(pt.rng_state(), ref.rng_array())
-    pt.set_head_groups(1)
-    pt.render(cam, spp, False, chunks=chunks)
-    assert pt.last_sample_groups == 0
-    ref.render(osc.camera, spp, False, chunks=chunks)
-    same(pt.accum(), ref.accum, f"{name} plain after head groups")

@@ -25,18 +25,6 @@ import pathtracercuda_amd as pa  # noqa: E402
 
 
 def apply(pt, tok, tiles):
-    h = re.fullmatch(r"([ht])(\d+)g(\d)", tok)          # head (tail) groups: the first (last) K positions in G groups
-    pt.set_head_groups((2 if h.group(1) == "h" else 3) if h else 0, int(h.group(2)) if h else 0,
-                       int(h.group(3)) if h else 0)
-    if h:
-        pt.set_companion(0)
-        pt.set_issue_priority(0)
-        return
-    c = re.fullmatch(r"c(\d)_(\d+)", tok)                # companion scheduling, mode and top positions
-    pt.set_companion(int(c.group(1)) if c else 0, int(c.group(2)) if c else 0)
-    if c:
-        pt.set_issue_priority(0)
-        return
     if tok in ("a", "o"):
         pt.set_issue_priority(0 if tok == "a" else 1)
         return
@@ -65,13 +53,10 @@ def main():
     ap.add_argument("--scheds", default="p0,p256")
     ap.add_argument("--rounds", type=int, default=3)
     ap.add_argument("--groups", type=int, default=1, help="sample groups: 1 = off, 0 = automatic")
-    ap.add_argument("--spans", action="store_true", help="record tile start/end times: the launch timeline")
     a = ap.parse_args()
     pt = (pa.Pathtracer(a.width, a.height, row_offset=0, row_stride=a.n, band_rows=8) if a.n > 1
           else pa.Pathtracer(a.width, a.height))
     pt.set_sample_groups(a.groups)
-    pt.set_tile_spans(a.spans)
-    lines = {}
     cam = pt.load_scene(a.scene)
     st = pt.rng_state()
     pt.render_raw(cam, 8, 2, True)                      # cost order
@@ -89,8 +74,6 @@ def main():
             if order is None:
                 order = np.argsort(-cost)[: max(1, cost.size // 100)]          # the first schedule's top 1 %
             tails[k].append((float(cost.max()), float(cost[order].mean()), float(cost.mean())))
-            if a.spans:
-                lines.setdefault(k, []).append(timeline(pt.tile_spans().reshape(-1, 2), cost))
             acc = pt.accum().view(np.uint32)
             if ref is None:
                 ref = acc.copy()
@@ -100,29 +83,7 @@ def main():
                       "groups": pt.last_sample_groups, "ms_min": {k: round(min(v), 2) for k, v in times.items()},
                       "ms_all": {k: [round(x, 2) for x in v] for k, v in times.items()},
                       "tile_ms_max_top1pct_mean": {k: [round(float(np.mean([t[i] for t in v])), 2) for i in range(3)]
-                                                   for k, v in tails.items()},
-                      "timeline": lines}), flush=True)
-
-
-def timeline(sp, cost):
-    """From the tiles' (start, end) ticks (100 MHz): when the last tile started and how many ran
-    then, the busy slot fraction of the launch, when the most expensive tile ended, and the active
-    tile count at tenths of the launch."""
-    s = sp[:, 0].astype(np.int64)
-    e = sp[:, 1].astype(np.int64)
-    t0 = s.min()
-    s, e = s - t0, e - t0
-    end = e.max()
-    last = s.max()
-    grid = np.linspace(0, end, 11)[1:-1]
-    active = [int(((s <= t) & (e > t)).sum()) for t in grid]
-    top = int(np.argmax(cost))
-    return {"launch_ms": round(end / 1e5, 2), "last_start_ms": round(last / 1e5, 2),
-            "running_at_last_start": int(((s <= last) & (e > last)).sum()),
-            "busy_fraction": round(float((e - s).sum()) / (5120.0 * end), 4),
-            "top_tile_end_ms": round(e[top] / 1e5, 2), "top_tile_start_ms": round(s[top] / 1e5, 2),
-            "tiles_ending_after_90pct": int((e > 0.9 * end).sum()),
-            "active_at_tenths": active}
+                                                   for k, v in tails.items()}}), flush=True)
 
 
 if __name__ == "__main__":
