@@ -728,35 +728,6 @@ PT_DEV bool walk_interior(const float4* __restrict__ cnodes, uint2* stack, const
     return false;
 }
 
-// The same walk with the pops folded into it (POPW, variant 42): a lane whose node misses both
-// children -- or whose leaf has been tested -- holds the pop word and pops one pending far child per
-// iteration of the one loop (re-tested against the current t_max, as before) instead of running a
-// nested pop loop: the pops of some lanes run beside the node visits of others, and the exec-mask
-// bookkeeping of a loop with a break inside a loop disappears from the scalar unit.  Each lane's
-// sequence of node tests, pushes, pops and re-tests is unchanged.  kPopWord cannot be a child word:
-// a leaf word has offset + count <= primitive count < 2^24.
-constexpr uint32_t kPopWord = 0xffffffffu;
-
-template <bool STATS, bool ALLFAST>
-PT_DEV bool walk_interior_popw(const float4* __restrict__ cnodes, uint2* stack, const SlabRay& R, uint32_t negMask,
-                               float tMin, float tMax, uint32_t& cur, uint32_t& sp, Counters& cnt)
-{
-    for (;;) {
-        if (cur == kPopWord) {
-            if (sp == 0u) return true;
-            const uint2 e = stack[64u * (--sp)];
-            if (tMax > __uint_as_float(e.y)) cur = e.x;
-            continue;
-        }
-        if ((cur >> 24) != 0u) return false;
-        if (STATS) { cnt.node_tests += 2; wave_tick(cnt.w_node); }
-        const ChildPair ch = cb_children<ALLFAST>(cnodes, cur, R, negMask, tMin, tMax);
-        stack[64u * sp] = make_uint2(ch.wF, __float_as_uint(ch.loF));
-        sp += ch.both ? 1u : 0u;
-        cur = ch.any ? ch.wNext : kPopWord;
-    }
-}
-
 template <bool STATS>
 PT_DEV uint32_t traverse_cb(const float4* __restrict__ cnodes, const float4* __restrict__ prims, uint2* stack,
                             const TraceParams& P, f3 o, f3 d, float& tHit, Counters& cnt)
@@ -964,7 +935,7 @@ PT_DEV void leaf_round_compact(const float4* __restrict__ prims, uint8_t* scr, u
 
 // The interior walk is walk_interior (the lean form: wave-uniform slab-form choice, unconditional
 // far-child write).  WW = 200 + EXITQ selects this traversal.
-template <bool STATS, int EXITQ, bool COMPACT = false, bool POPW = false>
+template <bool STATS, int EXITQ, bool COMPACT = false>
 PT_DEV bool traverse_cb_phase(const float4* __restrict__ cnodes, const float4* __restrict__ prims, uint2* stack,
                               const TraceParams& P, f3 o, f3 d, bool fresh, TravState& ts, Counters& cnt,
                               uint8_t* scr = nullptr)
@@ -1008,12 +979,8 @@ PT_DEV bool traverse_cb_phase(const float4* __restrict__ cnodes, const float4* _
     uint64_t tPhase = STATS ? __builtin_amdgcn_s_memtime() : 0;
     const bool allFast = __ballot(!R.fast) == 0;                         // wave-uniform
     while (!done) {
-        if (POPW)
-            done = allFast ? walk_interior_popw<STATS, true>(cnodes, stack, R, negMask, tMin, tMax, cur, sp, cnt)
-                           : walk_interior_popw<STATS, false>(cnodes, stack, R, negMask, tMin, tMax, cur, sp, cnt);
-        else
-            done = allFast ? walk_interior<STATS, true>(cnodes, stack, R, negMask, tMin, tMax, cur, sp, cnt)
-                           : walk_interior<STATS, false>(cnodes, stack, R, negMask, tMin, tMax, cur, sp, cnt);
+        done = allFast ? walk_interior<STATS, true>(cnodes, stack, R, negMask, tMin, tMax, cur, sp, cnt)
+                       : walk_interior<STATS, false>(cnodes, stack, R, negMask, tMin, tMax, cur, sp, cnt);
         if (STATS) wave_time(cnt.cyc_node, tPhase);
         if (done) break;
         uint32_t leafOff = cur & 0xffffffu, leafCnt = cur >> 24;
@@ -1033,10 +1000,7 @@ PT_DEV bool traverse_cb_phase(const float4* __restrict__ cnodes, const float4* _
             }
         }
         if (STATS) wave_time(cnt.cyc_leaf, tPhase);
-        if (POPW) {                                // the walk pops next (an empty stack ends now)
-            if (sp == 0u) { done = true; break; }
-            cur = kPopWord;
-        } else if (!pop()) { done = true; break; }
+        if (!pop()) { done = true; break; }
         // early exit once at most EXITQ/64 of the lanes that entered are still walking
         if ((uint32_t)__popcll(__ballot(1)) * 64u <= nAct * (uint32_t)EXITQ) break;
     }
@@ -1651,7 +1615,6 @@ __global__ void __launch_bounds__(WPB * 64, MINW) trace_kernel(TraceParams P)
     const uint32_t accL = 4u * sceneF4 + WPB * stackWords + wave * 192u + lane;   // float index
     // leaf compaction (WW / 100000): a pair list and a rank -> lane map per wave after the slices
     constexpr bool COMPACT = WW >= 100 && (WW / 100000) % 10 != 0;
-    constexpr bool POPW = WW >= 100 && (WW / 1000000) % 10 != 0;     // pops folded into the walk
     uint8_t* scr = COMPACT ? reinterpret_cast<uint8_t*>(lds4) + 4u * (4u * sceneF4 + WPB * stackWords + WPB * 192u) +
                                  wave * kCompactScratch
                            : nullptr;
@@ -1704,8 +1667,8 @@ __global__ void __launch_bounds__(WPB * 64, MINW) trace_kernel(TraceParams P)
                 if (STATS && fresh && !held) { cnt.segments++; wave_tick(cnt.w_segments); }
                 bool tdone = true;
                 if (!held) {
-                    tdone = traverse_cb_phase<STATS, WW % 100, COMPACT, POPW>(nodes, prims, reinterpret_cast<uint2*>(stack),
-                                                                               P, ps.o, ps.d, fresh, ts, cnt, scr);
+                    tdone = traverse_cb_phase<STATS, WW % 100, COMPACT>(nodes, prims, reinterpret_cast<uint2*>(stack), P,
+                                                                         ps.o, ps.d, fresh, ts, cnt, scr);
                     fresh = tdone;
                 }
                 if (DEFERQ > 0 || SKYQ > 0) {
@@ -2309,7 +2272,6 @@ static hipError_t launch_one(const TraceParams& P, hipStream_t stream)
 //       deferral, which costs a single pass of latency-bound waves 2.8 %
 //   48  small grids whose primitives fit in LDS too: records and primitives in LDS, 4 waves/SIMD,
 //       deferred hits
-//   42  variant 40 with the pops folded into the walk (walk_interior_popw); 43 the same for 41
 //   50  variant 40 with the leaf tests compacted across the round's lanes by shape family
 //   51  variant 41 with the same (leaf_round_compact; both measured, not defaults)
 constexpr int kV40Walk = 14212;     // variant 40's walk parameters (SKYQ 1, DEFERQ 4, exit <= 12/64;
@@ -2328,8 +2290,6 @@ static hipError_t launch_variant(int v, const TraceParams& P, hipStream_t stream
     case 46: return launch_one<STATS, 0, 4, 14212, 4, true, MODE>(P, stream);
     case 47: return launch_one<STATS, 1, 4, 224, 4, true, MODE>(P, stream);
     case 48: return launch_one<STATS, 2, 4, 13216, 4, true, MODE>(P, stream);
-    case 42: return launch_one<STATS, 1, 4, 1000000 + kV40Walk, 5, true, MODE>(P, stream);
-    case 43: return launch_one<STATS, 0, 4, 1000000 + 14212, 5, true, MODE>(P, stream);
     case 50: return launch_one<STATS, 1, 4, 100000 + kV40Walk, 5, true, MODE>(P, stream);
     case 51: return launch_one<STATS, 0, 4, 100000 + 14212, 5, true, MODE>(P, stream);
     default: return hipErrorInvalidValue;
@@ -2353,7 +2313,7 @@ static hipError_t launch_grouped(int v, const TraceParams& P, hipStream_t stream
 static bool variant_shipped(int v)
 {
     return v == 0 || v == 1 || v == 4 || v == 6 || v == 20 || v == 40 || v == 41 || v == 46 || v == 47 || v == 48 || v == 39 ||
-           v == 42 || v == 43 || v == 50 || v == 51;
+           v == 50 || v == 51;
 }
 
 // Cost pre-pass of a cold-start launch (render_impl): samples per pixel, and the smallest launch
