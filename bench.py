@@ -19,14 +19,14 @@ N GPUs, two launch modes, one partition (8-row bands, band b -> GPU b mod N):
     unpermute kernel -- the boundary that replaces Pathtracer.cpp:40's single device); the timed
     step is pt_group_render + pt_group_gather.  Fewer than N visible GPUs is an error (exit 2);
     `--group 1` runs this path at N = 1 too.
-Scaling.  The path is partitioned (pixels are independent; the only exchange is the one framebuffer
-gather), so the headline is weak scaling (the task's rule for partitioned paths): every
-GPU keeps one C3 frame's worth of pixels -- the image grows by sqrt(N) per axis (N = 4: 3840x2160,
-C4's image, at 1024 spp) -- and value = all samples / step time.  At N > 1 a strong-scaling record
-of the fixed 1920x1080 image is added beside it (`secondary`), so both are on the driver's clock;
-`--scaling strong` makes the fixed image the headline.  At N = 1 the two coincide, and the C2 and C5
-workloads are added as secondary records, each with its roofline and CPU baseline (`--extra ''` drops
-C5, `--secondary 0` turns all secondary records off).
+Scaling.  The headline is the metric's own workload at every N: strong scaling of the fixed
+1920x1080 x 1024 spp image (BASELINE.json metric "1080p 1024spp, 1/2/4/8 MI355X"), value = all
+samples / the slowest rank's step time.  At N > 1 a weak-scaling record is added beside it
+(`secondary`: every GPU keeps one C3 frame's worth of pixels, the image grows by sqrt(N) per axis),
+so both are on the driver's clock; `--scaling weak` swaps them.  At N = 1 the two coincide, and the
+secondary records are the reference's unchanged call loop on C3 (128 separate render(cam, 8, i == 0)
+calls through the drop-in Pathtracer, main.cpp:272-279), C2 and C5, each C2/C5 with its roofline and
+CPU baseline (`--extra ''` drops C5, `--secondary 0` turns all secondary records off).
 
 Printed JSON line (rank 0): value = samples of the whole workload / step time.  roofline: the
 trace kernel is bound by VALU issue -- achieved = its wave64 VALU instructions per
@@ -74,8 +74,8 @@ def parse_args(argv=None):
     p.add_argument("--warmup", type=int, default=1)
     p.add_argument("--config", choices=sorted(CONFIGS), default="C3")
     p.add_argument("--spp", type=int, default=0, help="override the config's spp (multiple of 8)")
-    p.add_argument("--scaling", choices=["weak", "strong"], default="weak",
-                   help="strong: the same workload for every N (default); weak: the image grows by sqrt(N) per axis")
+    p.add_argument("--scaling", choices=["weak", "strong"], default="strong",
+                   help="strong (default): the same 1080p workload for every N; weak: the image grows by sqrt(N) per axis")
     p.add_argument("--band-rows", type=int, default=8, help="rows per band of the multi-GPU partition")
     p.add_argument("--secondary", type=int, default=1,
                    help="N=1: add the C2 and --extra records; N>1: add the other scaling mode's record")
@@ -95,7 +95,8 @@ def resolve_mode(gpus: int, world: int, group: int, visible) -> str:
     the number of visible GPUs (queried only for the group path).  Never silently runs fewer GPUs
     than asked: a mismatch raises SystemExit(2) with the reason."""
     if gpus < 1:
-        raise SystemExit("bench.py: --gpus must be >= 1")
+        print("bench.py: --gpus must be >= 1", file=sys.stderr)
+        raise SystemExit(2)
     if world > 1:
         if gpus not in (1, world):
             print(f"bench.py: --gpus {gpus} but WORLD_SIZE={world}", file=sys.stderr)
@@ -137,12 +138,20 @@ def algorithmic_bytes(stats: dict) -> float:
 
 
 def kernel_source_sha() -> str:
-    """sha256 (16 hex) of the kernel sources the trace kernel is built from: a committed PMC profile
-    records the same digest, so a profile of another kernel cannot pair with this build unnoticed."""
+    """sha256 (16 hex) of what the trace kernel is built from -- its sources, the headers under
+    include/ and the hipcc flags of the Makefile (HIPFLAGS; e.g. -fno-slp-vectorize moved C3 by
+    4.6 %): a committed PMC profile records the same digest, so a profile of another binary cannot
+    pair with this build unnoticed."""
     import hashlib
+    import re
     h = hashlib.sha256()
     for f in ("pathtracercuda_amd/csrc/pt_kernels.hip", "pathtracercuda_amd/csrc/pt_math.h"):
         h.update((ROOT / f).read_bytes())
+    for f in sorted((ROOT / "include").glob("*.h")):
+        h.update(f.read_bytes())
+    mk = (ROOT / "Makefile").read_text()
+    m = re.search(r"^HIPFLAGS \?=(.*?)(?<!\\)\n", mk, re.S | re.M)
+    h.update((m.group(1) if m else "").encode())
     return h.hexdigest()[:16]
 
 
@@ -287,10 +296,26 @@ class Run:
         self.pt.close()
 
 
-def timed(run, steps, warmup, local_rank, dist_on):
-    if run.mode == "group":
-        # pt_group_render and pt_group_gather return after every device's stream is idle (and this
-        # process does not load torch: see main), so the group's calls are their own barrier
+class CallLoopRun(Run):
+    """The reference's headless loop unchanged (main.cpp:272-279): spp / 8 separate
+    Pathtracer::render(camera, 8, i == 0) calls per step through the C++ drop-in (libpt_host ->
+    pt_render: one launch per call, synchronous like Pathtracer.cpp:162-227).  step() returns the
+    sum of getTiming() over the calls -- the loop's totalGpuTime."""
+
+    def step(self):
+        total = 0.0
+        for i in range(self.chunks):
+            self.pt.render(self.cam, CHUNK, i == 0)
+            total += self.pt.get_timing()
+        return total
+
+
+def timed(run, steps, warmup, local_rank, dist_on, use_torch=True):
+    if not use_torch:
+        # the in-process device group (main): pt_group_render / pt_group_gather return after every
+        # device's stream is idle, and so does pt_render on a plain context (hipEventSynchronize),
+        # so the calls are their own barrier -- and this process must not load torch (two HIP
+        # runtimes, INTEGRATION.md §4)
         def barrier_sync():
             pass
     else:
@@ -433,9 +458,10 @@ def main():
         dist.all_reduce(t)
         return dict(zip(keys, [float(x) for x in t]))
 
+    use_torch = mode != "group"        # decided by the process's launch mode, for every record below
     run = Run(cfg, W, H, spp, rank, n, local_rank, args.band_rows, mode)
     st = stats_all(run.instrument())
-    elapsed, kernel_ms = timed(run, args.steps, args.warmup, local_rank, dist_on)
+    elapsed, kernel_ms = timed(run, args.steps, args.warmup, local_rank, dist_on, use_torch)
     main_rec = record(cfg, run, elapsed, kernel_ms, args.steps, st, n)
     gather_ms = run.gather_ms
     run.close()
@@ -467,12 +493,26 @@ def main():
     if args.secondary:
         if n == 1:
             recs = []
+            if args.config == "C3":
+                # the reference's unchanged call loop on the headline workload
+                rl = CallLoopRun(cfg, W, H, spp, 0, 1, local_rank, 1, "single")
+                el, kl = timed(rl, args.steps, args.warmup, local_rank, False, use_torch)
+                rl.close()
+                recs.append({"label": "C3 call loop", "value": round(W * H * spp * args.steps / el / 1e6, 3),
+                             "unit": "Msamples/s", "ms_per_step": round(el * 1e3 / args.steps, 3),
+                             "gpu_ms_per_step": round(kl / args.steps, 3),
+                             "fused_over_loop": round(el / elapsed, 4),
+                             "workload": workload_name(cfg, W, H, spp) + " as " + str(spp // CHUNK) + " render() calls",
+                             "what": "main.cpp:272-279 unchanged: Pathtracer::render(cam, 8, i == 0) per call, one "
+                                     "synchronous launch each (libpt_host -> pt_render); gpu_ms_per_step = sum of "
+                                     "getTiming() (the loop's totalGpuTime); fused_over_loop = loop step time / "
+                                     "headline (one chunked launch) step time"})
             for label in ("C2",) + tuple(x for x in args.extra.split(",") if x):
                 c2 = CONFIGS[label]
                 r2 = Run(c2, c2["width"], c2["height"], c2["spp"], 0, 1, local_rank, 1, "single")
                 st2 = r2.instrument()
                 k2steps = max(args.steps, 20) if label == "C2" else args.steps   # C2: 4.4 ms steps
-                e2, k2 = timed(r2, k2steps, args.warmup, local_rank, False)
+                e2, k2 = timed(r2, k2steps, args.warmup, local_rank, False, use_torch)
                 rec2 = record(c2, r2, e2, k2, k2steps, st2, 1)
                 r2.close()
                 rec2["label"] = label
@@ -488,7 +528,7 @@ def main():
                 Hw = int(round(cfg["height"] * math.sqrt(n) / 8.0)) * 8
             rw = Run(cfg, Ww, Hw, spp, rank, n, local_rank, args.band_rows, mode)
             stw = stats_all(rw.instrument())
-            ew, kw = timed(rw, min(args.steps, 3), 1, local_rank, dist_on)
+            ew, kw = timed(rw, min(args.steps, 3), 1, local_rank, dist_on, use_torch)
             recw = record(cfg, rw, ew, kw, min(args.steps, 3), stw, n)
             rw.close()
             recw["label"] = (f"{args.config} weak scaling (image {Ww}x{Hw}: one {cfg['width']}x{cfg['height']} frame per GPU)"

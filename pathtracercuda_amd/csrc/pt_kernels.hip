@@ -299,87 +299,6 @@ PT_DEV bool prim_hit(const float4* __restrict__ prims, uint32_t p, f3 o, f3 d, f
     return prim_hit_rec(load_prim(prims, p), o, d, tMin, tMax, tOut);
 }
 
-// The same test split at t_max (leaf compaction, variant 50): everything that does not depend on
-// t_max is computed first -- possibly on another lane -- and the accept predicate of prim_hit_rec
-// is applied afterwards by the ray's own lane, in primitive order with its running t_max.
-// f: bits 0-1 kind (0 plane, 1 cube, 2 sphere, 3 other quadric), bit 2 the t_max-free conditions
-// hold, bits 3-4 the t_max-free halves of the two roots' validity (other quadrics).
-struct PrimCand {
-    float a, b;
-    uint32_t f;
-};
-
-PT_DEV PrimCand prim_cand(const PrimRec& q, uint32_t family, f3 o, f3 d, float tMin)
-{
-    const LocalRay r = to_local(q.r0, q.r1, q.r2, o, d);
-    PrimCand c = {0.0f, 0.0f, 0u};
-    if (family == 0u) {                                    // disk, quad: accept iff ok && !(t > tMax)
-        const float t = -r.o.y / r.d.y;
-        const float hx = r.o.x + r.d.x * t;
-        const float hz = r.o.z + r.d.z * t;
-        const bool in = q.type == QUAD ? !(fabsf(hx) > 1.0f || fabsf(hz) > 1.0f) : !((hx * hx + hz * hz) >= 1.0f);
-        c.a = t;
-        c.f = (r.d.y != 0.0f && !(t <= tMin) && in) ? 4u : 0u;
-    } else if (family == 1u) {                             // cube: hi = min(tMax, m), accept iff !(hi <= lo)
-        float lo = tMin, m = __builtin_inff();
-        const float ox[3] = {r.o.x, r.o.y, r.o.z};
-        const float dx[3] = {r.d.x, r.d.y, r.d.z};
-#pragma unroll
-        for (int a = 0; a < 3; ++a) {
-            const float invD = rcp_rn(dx[a]);
-            float t0 = (-1.0f - ox[a]) * invD;
-            float t1 = (1.0f - ox[a]) * invD;
-            if (invD < 0.0f) { const float tmp = t0; t0 = t1; t1 = tmp; }
-            lo = t0 > lo ? t0 : lo;
-            m = t1 < m ? t1 : m;
-        }
-        c.a = lo;
-        c.b = m;
-        c.f = 1u | 4u;
-    } else {                                               // quadrics
-        float t0 = 0.0f, t1 = 0.0f;
-        const bool ok = quadric_roots(q.type, r, t0, t1) && !(t1 <= tMin);
-        c.a = t0;
-        if (q.type == SPHERE) {
-            c.b = t0 > tMin ? t0 : t1;
-            c.f = 2u | (ok ? 4u : 0u);
-        } else {
-            const float h0 = r.d.y * t0 + r.o.y;
-            const float h1 = r.d.y * t1 + r.o.y;
-            const bool v0 = t0 > tMin && h0 >= -1.0f && h0 <= 1.0f;
-            const bool v1 = t1 > tMin && h1 >= -1.0f && h1 <= 1.0f;
-            c.b = t1;
-            c.f = 3u | (ok ? 4u : 0u) | (v0 ? 8u : 0u) | (v1 ? 16u : 0u);
-        }
-    }
-    return c;
-}
-
-// prim_hit_rec's verdict from a candidate and the running t_max.  The cube's sequential clip
-// hi = min(tMax, t1x, t1y, t1z) (NaN t1 skipped, a NaN t_max kept) equals (m < tMax ? m : tMax).
-PT_DEV bool cand_accept(const PrimCand& c, float tMax, float& tOut)
-{
-    const uint32_t kind = c.f & 3u;
-    const bool le = !(c.a > tMax);
-    bool acc;
-    float t;
-    if (kind == 1u) {
-        const float hi = c.b < tMax ? c.b : tMax;
-        acc = !(hi <= c.a);
-        t = c.a;
-    } else if (kind == 3u) {
-        const bool v0 = (c.f & 8u) != 0u && c.a <= tMax;
-        const bool v1 = (c.f & 16u) != 0u && c.b <= tMax;
-        acc = le && (v0 || v1);
-        t = v0 ? c.a : c.b;
-    } else {
-        acc = le;
-        t = kind == 2u ? c.b : c.a;
-    }
-    tOut = t;
-    return (c.f & 4u) != 0u && acc;
-}
-
 struct Counters {
     uint32_t node_tests, prim_tests, hits, sky, segments, samples;
     // wave-level executions of the same points (SIMD efficiency = lane count / (64 * wave count))
@@ -811,134 +730,11 @@ struct TravState {
     float tMax;
 };
 
-// Leaf compaction (variant 50).  The lanes of a leaf round hold 1-4 pending
-// primitives each, of up to three shape families (plane / cube / quadric code paths of the test).
-// The round's (lane, primitive) pairs are numbered family-major (then position, then lane) with
-// ballots and mbcnt, written as one byte each (owner lane, position) to a per-wave LDS list, and
-// processed in batches of as many pairs as the round has lanes: the lane of rank r in batch b takes
-// pair b * lanes + r, fetches the owner's ray and leaf offset with ds_bpermute and computes the
-// t_max-free candidate (prim_cand) -- each family's path runs once per batch on a contiguous run
-// of lanes.  Each owner then pulls its candidates back (ds_bpermute from the computing lane, found
-// through a rank -> lane byte map) and accepts them in primitive order with its running t_max, so
-// ties, the sphere's far root and NaNs resolve exactly as in the in-order loop.  Rounds with more
-// than two batches of pairs, or a leaf of more than 4 primitives, run the in-order loop.
-constexpr uint32_t kCompactList = 128;                 // pair-list bytes per wave
-constexpr uint32_t kCompactScratch = kCompactList + 64; // + the rank -> lane map
-
-PT_DEV uint32_t lanes_below(uint64_t m)
-{
-    return __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
-}
-
-PT_DEV float bperm_f(int src, float v) { return __int_as_float(__builtin_amdgcn_ds_bpermute(src, __float_as_int(v))); }
-PT_DEV uint32_t bperm_u(int src, uint32_t v) { return (uint32_t)__builtin_amdgcn_ds_bpermute(src, (int)v); }
-
-template <bool STATS>
-PT_DEV void leaf_round_compact(const float4* __restrict__ prims, uint8_t* scr, uint32_t leafOff, uint32_t leafCnt,
-                               f3 o, f3 d, float tMin, float& tMax, uint32_t& elem, Counters& cnt)
-{
-    const uint32_t lane = threadIdx.x & 63u;
-    // family of each position of the leaf (pt_set_scene: bit 4F + k), bit 31 for leaves of > 4
-    const uint32_t fw = __float_as_uint(prims[4 * leafOff + 3].y);
-    const uint64_t ex = __ballot(1);
-    const uint32_t A = (uint32_t)__popcll(ex);
-    uint32_t slots = 0, N = 0, fs1 = 0, fs2 = 0;
-    bool fits = __ballot((fw >> 31) != 0u) == 0ull;
-    if (fits) {
-#pragma unroll
-        for (uint32_t F = 0; F < 3; ++F) {
-            if (F == 1) fs1 = N;
-            if (F == 2) fs2 = N;
-#pragma unroll
-            for (uint32_t k = 0; k < 4; ++k) {
-                const bool mine = ((fw >> (4 * F + k)) & 1u) != 0u;
-                const uint64_t M = __ballot(mine);
-                if (M == 0ull) continue;
-                if (mine) {
-                    const uint32_t sl = N + lanes_below(M);
-                    slots |= sl << (8 * k);
-                    if (sl < kCompactList) scr[sl] = (uint8_t)(lane | (k << 6));
-                }
-                N += (uint32_t)__popcll(M);
-            }
-        }
-        fits = N <= 2 * A && N <= kCompactList;
-    }
-    if (!fits) {
-        while (leafCnt > 0) {
-            if (STATS) { cnt.prim_tests++; wave_tick(cnt.w_prim); leaf_position_stats(prims, leafOff, cnt); }
-            float t;
-            if (prim_hit(prims, leafOff, o, d, tMin, tMax, t)) {
-                tMax = t;
-                elem = leafOff;
-            }
-            ++leafOff;
-            --leafCnt;
-        }
-        return;
-    }
-    const uint32_t rank = lanes_below(ex);
-    scr[kCompactList + rank] = (uint8_t)lane;
-    __builtin_amdgcn_wave_barrier();
-    PrimCand c0 = {0.0f, 0.0f, 0u}, c1 = {0.0f, 0.0f, 0u};
-#pragma unroll
-    for (uint32_t b = 0; b < 2; ++b) {
-        if (b * A >= N) break;                              // wave-uniform
-        const uint32_t sl = b * A + rank;
-        const bool act = sl < N;
-        const uint32_t e = scr[act ? sl : 0u];
-        const int src = (int)((e & 63u) << 2);
-        const uint32_t p = bperm_u(src, leafOff) + (e >> 6);
-        f3 oo, dd;
-        oo.x = bperm_f(src, o.x);
-        oo.y = bperm_f(src, o.y);
-        oo.z = bperm_f(src, o.z);
-        dd.x = bperm_f(src, d.x);
-        dd.y = bperm_f(src, d.y);
-        dd.z = bperm_f(src, d.z);
-        const uint32_t F = (sl >= fs1 ? 1u : 0u) + (sl >= fs2 ? 1u : 0u);
-        if (STATS) {
-            if (act) cnt.prim_tests++;
-            wave_tick(cnt.w_prim);
-            const uint32_t fam = (__ballot(act && F == 0u) != 0ull) + (__ballot(act && F == 1u) != 0ull) + (__ballot(act && F == 2u) != 0ull);
-            if (lane == (uint32_t)(__ffsll((long long)ex) - 1)) cnt.w_fam_exec += fam;
-        }
-        PrimCand r = {0.0f, 0.0f, 0u};
-        if (act) r = prim_cand(load_prim(prims, p), F, oo, dd, tMin);
-        if (b == 0) c0 = r;
-        else c1 = r;
-    }
-    const bool two = N > A;                                 // wave-uniform
-#pragma unroll
-    for (uint32_t k = 0; k < 4; ++k) {
-        if (__ballot(k < leafCnt) == 0ull) break;           // every lane stays active for the bpermutes
-        const uint32_t sl = (slots >> (8 * k)) & 0xffu;
-        const bool hi = sl >= A;
-        const uint32_t cl = scr[kCompactList + (k < leafCnt ? (hi ? sl - A : sl) : 0u)];
-        const int src = (int)(cl << 2);
-        PrimCand c;
-        c.a = bperm_f(src, c0.a);
-        c.b = bperm_f(src, c0.b);
-        c.f = bperm_u(src, c0.f);
-        if (two) {
-            const float a1 = bperm_f(src, c1.a), b1 = bperm_f(src, c1.b);
-            const uint32_t f1 = bperm_u(src, c1.f);
-            if (hi) { c.a = a1; c.b = b1; c.f = f1; }
-        }
-        float t;
-        if (k < leafCnt && cand_accept(c, tMax, t)) {
-            tMax = t;
-            elem = leafOff + k;
-        }
-    }
-}
-
 // The interior walk is walk_interior (the lean form: wave-uniform slab-form choice, unconditional
 // far-child write).  WW = 200 + EXITQ selects this traversal.
-template <bool STATS, int EXITQ, bool COMPACT = false>
+template <bool STATS, int EXITQ>
 PT_DEV bool traverse_cb_phase(const float4* __restrict__ cnodes, const float4* __restrict__ prims, uint2* stack,
-                              const TraceParams& P, f3 o, f3 d, bool fresh, TravState& ts, Counters& cnt,
-                              uint8_t* scr = nullptr)
+                              const TraceParams& P, f3 o, f3 d, bool fresh, TravState& ts, Counters& cnt)
 {
     const float tMin = 0.001f;
     SlabRay R;
@@ -985,19 +781,15 @@ PT_DEV bool traverse_cb_phase(const float4* __restrict__ cnodes, const float4* _
         if (done) break;
         uint32_t leafOff = cur & 0xffffffu, leafCnt = cur >> 24;
         if (STATS) leaf_round_stats(prims, leafOff, leafCnt, cnt);
-        if (COMPACT) {
-            leaf_round_compact<STATS>(prims, scr, leafOff, leafCnt, o, d, tMin, tMax, elem, cnt);
-        } else {
-            while (leafCnt > 0) {
-                if (STATS) { cnt.prim_tests++; wave_tick(cnt.w_prim); leaf_position_stats(prims, leafOff, cnt); }
-                float t;
-                if (prim_hit(prims, leafOff, o, d, tMin, tMax, t)) {
-                    tMax = t;
-                    elem = leafOff;
-                }
-                ++leafOff;
-                --leafCnt;
+        while (leafCnt > 0) {
+            if (STATS) { cnt.prim_tests++; wave_tick(cnt.w_prim); leaf_position_stats(prims, leafOff, cnt); }
+            float t;
+            if (prim_hit(prims, leafOff, o, d, tMin, tMax, t)) {
+                tMax = t;
+                elem = leafOff;
             }
+            ++leafOff;
+            --leafCnt;
         }
         if (STATS) wave_time(cnt.cyc_leaf, tPhase);
         if (!pop()) { done = true; break; }
@@ -1613,11 +1405,6 @@ __global__ void __launch_bounds__(WPB * 64, MINW) trace_kernel(TraceParams P)
     const uint32_t stackWords = (WW >= 3 ? 2u : 1u) * P.stackDepth * 64u;
     uint32_t* stack = ldsStacks + wave * stackWords + (WW >= 3 ? 2u : 1u) * lane;
     const uint32_t accL = 4u * sceneF4 + WPB * stackWords + wave * 192u + lane;   // float index
-    // leaf compaction (WW / 100000): a pair list and a rank -> lane map per wave after the slices
-    constexpr bool COMPACT = WW >= 100 && (WW / 100000) % 10 != 0;
-    uint8_t* scr = COMPACT ? reinterpret_cast<uint8_t*>(lds4) + 4u * (4u * sceneF4 + WPB * stackWords + WPB * 192u) +
-                                 wave * kCompactScratch
-                           : nullptr;
     Counters cnt = {};
     uint32_t slot = PERSIST ? wave_fetch(P.tileCursor, 1u) : __builtin_amdgcn_readfirstlane(blockIdx.x * (uint32_t)WPB + wave);
     for (;;) {
@@ -1667,8 +1454,8 @@ __global__ void __launch_bounds__(WPB * 64, MINW) trace_kernel(TraceParams P)
                 if (STATS && fresh && !held) { cnt.segments++; wave_tick(cnt.w_segments); }
                 bool tdone = true;
                 if (!held) {
-                    tdone = traverse_cb_phase<STATS, WW % 100, COMPACT>(nodes, prims, reinterpret_cast<uint2*>(stack), P,
-                                                                         ps.o, ps.d, fresh, ts, cnt, scr);
+                    tdone = traverse_cb_phase<STATS, WW % 100>(nodes, prims, reinterpret_cast<uint2*>(stack), P,
+                                                                ps.o, ps.d, fresh, ts, cnt);
                     fresh = tdone;
                 }
                 if (DEFERQ > 0 || SKYQ > 0) {
@@ -2203,8 +1990,7 @@ static hipError_t launch_one(const TraceParams& P, hipStream_t stream)
 {
     const size_t nodeF4 = WW >= 3 ? 4 * (size_t)P.cnodeCount : 2 * (size_t)P.nodeCount;
     const size_t sceneBytes = ((SL >= 1 ? nodeF4 : 0) + (SL >= 2 ? 4 * (size_t)P.primCount : 0)) * sizeof(float4);
-    const size_t lds = sceneBytes + (size_t)WPB * P.stackDepth * 64 * (WW >= 3 ? 8 : 4) + (size_t)WPB * 64 * 12 +
-                       (WW >= 100 && (WW / 100000) % 10 != 0 ? (size_t)WPB * kCompactScratch : 0);
+    const size_t lds = sceneBytes + (size_t)WPB * P.stackDepth * 64 * (WW >= 3 ? 8 : 4) + (size_t)WPB * 64 * 12;
     if (WW >= 3 && P.cnodes == nullptr) return MODE == 1 ? hipErrorInvalidValue : launch_one<STATS, SL, WPB, 1, MINW, PERSIST, MODE>(P, stream);  // no child-box layout
     if (lds > 160 * 1024) {
         // scene too large to stage in LDS: the same variant reading the scene through the caches
@@ -2272,8 +2058,8 @@ static hipError_t launch_one(const TraceParams& P, hipStream_t stream)
 //       deferral, which costs a single pass of latency-bound waves 2.8 %
 //   48  small grids whose primitives fit in LDS too: records and primitives in LDS, 4 waves/SIMD,
 //       deferred hits
-//   50  variant 40 with the leaf tests compacted across the round's lanes by shape family
-//   51  variant 41 with the same (leaf_round_compact; both measured, not defaults)
+// Variants 50/51 (leaf tests compacted across a round's lanes by shape family, -14.6 % on C3) were
+// measured in round 3 and removed in round 4; commit 1b0d322 has them.
 constexpr int kV40Walk = 14212;     // variant 40's walk parameters (SKYQ 1, DEFERQ 4, exit <= 12/64;
                                     // retuned in round 3, profiles/r03_walk_params_ab.json)
 template <bool STATS, int MODE = 0>
@@ -2290,8 +2076,6 @@ static hipError_t launch_variant(int v, const TraceParams& P, hipStream_t stream
     case 46: return launch_one<STATS, 0, 4, 14212, 4, true, MODE>(P, stream);
     case 47: return launch_one<STATS, 1, 4, 224, 4, true, MODE>(P, stream);
     case 48: return launch_one<STATS, 2, 4, 13216, 4, true, MODE>(P, stream);
-    case 50: return launch_one<STATS, 1, 4, 100000 + kV40Walk, 5, true, MODE>(P, stream);
-    case 51: return launch_one<STATS, 0, 4, 100000 + 14212, 5, true, MODE>(P, stream);
     default: return hipErrorInvalidValue;
     }
 }
@@ -2312,8 +2096,7 @@ static hipError_t launch_grouped(int v, const TraceParams& P, hipStream_t stream
 
 static bool variant_shipped(int v)
 {
-    return v == 0 || v == 1 || v == 4 || v == 6 || v == 20 || v == 40 || v == 41 || v == 46 || v == 47 || v == 48 || v == 39 ||
-           v == 50 || v == 51;
+    return v == 0 || v == 1 || v == 4 || v == 6 || v == 20 || v == 40 || v == 41 || v == 46 || v == 47 || v == 48 || v == 39;
 }
 
 // Cost pre-pass of a cold-start launch (render_impl): samples per pixel, and the smallest launch
@@ -2533,26 +2316,13 @@ PT_API int pt_set_scene(pt_context* ctx, const pt_bvh_node* nodes, uint32_t node
         q[2] = make_float4(R.aabb_min[0], R.aabb_max[0], R.aabb_min[1], R.aabb_max[1]);
         q[3] = make_float4(u2f(word(i + 1)), u2f(word(nodes[i].offset)), u2f(1u << ((nodes[i].primitive_count_axis >> 8) & 0xffu)), 0.0f);
     }
-    // hp[4 * off + 3].y of a leaf's first primitive: bit 4F + k when position k has shape family F
-    // (0 disk/quad, 1 cube, 2 quadric), bit 31 for leaves of more than 4 (leaf compaction)
-    std::vector<uint32_t> famWord(prim_count, 0u);
-    for (uint32_t i = 0; i < node_count; ++i) {
-        const uint32_t count = nodes[i].primitive_count_axis >> 16, off = nodes[i].offset;
-        if (count == 0 || (uint64_t)off + count > prim_count) continue;
-        if (count > 4 || famWord[off] != 0u) { famWord[off] = 1u << 31; continue; }   // (or two leaves share a start)
-        for (uint32_t k = 0; k < count; ++k) {
-            const uint32_t t = prims[off + k].type;
-            const uint32_t F = (t == DISK || t == QUAD) ? 0u : (t == CUBE ? 1u : 2u);
-            famWord[off] |= 1u << (4 * F + k);
-        }
-    }
     for (uint32_t i = 0; i < prim_count; ++i) {
         const pt_hittable& h = prims[i];
         const float(&R)[3][4] = h.inv_transform_rows;
         hp[4 * i + 0] = make_float4(R[0][0], R[1][0], R[0][1], R[1][1]);
         hp[4 * i + 1] = make_float4(R[0][2], R[1][2], R[0][3], R[1][3]);
         hp[4 * i + 2] = make_float4(R[2][0], R[2][1], R[2][2], R[2][3]);
-        hp[4 * i + 3] = make_float4(u2f(h.type), u2f(famWord[i]), 0.0f, 0.0f);
+        hp[4 * i + 3] = make_float4(u2f(h.type), 0.0f, 0.0f, 0.0f);
         hm[3 * i] = make_float4(h.base_color[0], h.base_color[1], h.base_color[2], h.roughness);
         hm[3 * i + 1] = make_float4(h.emissive[0], h.emissive[1], h.emissive[2], h.metalness);
         hm[3 * i + 2] = make_float4(u2f(h.texture_index), u2f(h.material_type), 0.0f, 0.0f);
@@ -2944,7 +2714,14 @@ static int render_impl(pt_context* ctx, const pt_camera* cam, uint32_t spp, uint
     P.tileCursor = ctx->tileCursor;
     P.numSlots = tiles;
     P.occCap = ctx->occupancy;
-    issue_priority(ctx, tiles, P.prio);
+    // Issue priority follows the order position, so it is meaningful only on a current cost order.
+    // A launch whose tile costs will rebuild the order (stale order, or this launch measures >= 4x
+    // the samples the order came from; see the rebuild below) runs without it: graded priority
+    // shortens the head quarter's tiles, and costs measured under it would rank those tiles lower
+    // on every rebuild (a feedback the order would carry over camera moves).
+    const bool rebuilds = ctx->schedule == 0 &&
+                          (ctx->orderStale || !ctx->orderValid || (uint64_t)spp * chunks >= 4 * ctx->orderSamples);
+    if (!rebuilds || ctx->prioMode == 2) issue_priority(ctx, tiles, P.prio);   // explicit bounds: always
     if (stats) PT_HIP_CHECK(ctx, hipMemsetAsync(ctx->stats, 0, kStatWords * sizeof(unsigned long long), ctx->stream));
     int variant = pick_variant(ctx);
     // speculative sample groups
@@ -2966,6 +2743,20 @@ static int render_impl(pt_context* ctx, const pt_camera* cam, uint32_t spp, uint
     ctx->lastGroups = 0;
     memset(ctx->groupStats, 0, sizeof(ctx->groupStats));
     ++ctx->epoch;
+    uint32_t ssgCap = 0;
+    if (G) {
+        const uint32_t ssgN = total / G;
+        // an item runs its group and, where the next group's guess missed, into the group after it;
+        // further dead ends go to patch rounds
+        ssgCap = std::min<uint32_t>({total, 2 * ssgN + 64, 10000u});   // end offsets: 16-bit draw pairs (<= 6 per sample)
+        const size_t J = 2 * (size_t)G - 1;
+        if (!ssg_reserve(ctx, tiles, (size_t)tiles * J, (size_t)tiles * J * ssgCap, (size_t)tiles * ssgCap,
+                         (size_t)tiles * J * ssg_window_words(G, ssgN)))
+            G = 0;
+    }
+    // a plain launch after grouped ones releases the group logs (a stream synchronisation and frees
+    // of up to ~15 GB): before the timed region starts
+    if (!G) ssg_release(ctx);
     PT_HIP_CHECK(ctx, hipEventRecord(ctx->ev0, ctx->stream));
     if (sorted && (ctx->orderStale || !ctx->orderValid) && (uint64_t)spp * chunks >= kPrepassMinSpp && !stats) {
         // Cold start (first launch, or the scene, a texture or the camera changed): a short cost
@@ -2979,6 +2770,7 @@ static int render_impl(pt_context* ctx, const pt_camera* cam, uint32_t spp, uint
         Q.ignoreFirst = 1;
         Q.discard = 1;
         Q.order = ctx->rowMajor;
+        for (int i = 0; i < 3; ++i) Q.prio[i] = 0;        // row-major positions: no priority grading
         Q.pairsOut = guesses && ssg_reserve(ctx, tiles, 0, 0, 0) ? ctx->pairs : nullptr;
         if (Q.pairsOut) ctx->pairsValid = true;
         PT_HIP_CHECK(ctx, Q.pairsOut ? launch_grouped<2>(variant, Q, ctx->stream) : launch_variant<false>(variant, Q, ctx->stream));
@@ -2986,18 +2778,6 @@ static int render_impl(pt_context* ctx, const pt_camera* cam, uint32_t spp, uint
         if (rs != PT_OK) return rs;
         P.order = ctx->order;
     }
-    uint32_t ssgCap = 0;
-    if (G) {
-        const uint32_t ssgN = total / G;
-        // an item runs its group and, where the next group's guess missed, into the group after it;
-        // further dead ends go to patch rounds
-        ssgCap = std::min<uint32_t>({total, 2 * ssgN + 64, 10000u});   // end offsets: 16-bit draw pairs (<= 6 per sample)
-        const size_t J = 2 * (size_t)G - 1;
-        if (!ssg_reserve(ctx, tiles, (size_t)tiles * J, (size_t)tiles * J * ssgCap, (size_t)tiles * ssgCap,
-                         (size_t)tiles * J * ssg_window_words(G, ssgN)))
-            G = 0;
-    }
-    if (!G) ssg_release(ctx);
     if (G && P.tileCost) PT_HIP_CHECK(ctx, hipMemsetAsync(P.tileCost, 0, (size_t)tiles * sizeof(uint32_t), ctx->stream));
     if (G) {
         const int rc = run_groups(ctx, variant, P, G, tiles, ssgCap, ctx->stream);

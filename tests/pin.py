@@ -36,6 +36,29 @@ def pin_mask() -> np.ndarray:
     return np.kron(mb, np.ones((32, 32), bool))
 
 
+def mask_distance() -> np.ndarray:
+    """Per 32 x 32 block: Chebyshev distance in blocks to the nearest masked block (0 = masked)."""
+    mb = pin_mask()[::32, ::32]
+    iy, ix = np.nonzero(~mb)
+    yy, xx = np.mgrid[0:mb.shape[0], 0:mb.shape[1]]
+    d = np.maximum(np.abs(yy[..., None] - iy), np.abs(xx[..., None] - ix)).min(-1)
+    return d
+
+
+def bias_by_ring(x: np.ndarray, ref: np.ndarray, m: np.ndarray) -> list:
+    """Mean (x - ref) per channel over the unmasked pixels of the blocks at each distance from the
+    masked earth sphere (its light is missing from our render: the reference's earth.png is absent,
+    so our sphere is untextured white, cornell_box.json:136-141, Material.inl:26-34)."""
+    dist = np.kron(mask_distance(), np.ones((32, 32), int))
+    d = (x - ref).astype(np.float64)
+    out = []
+    for r in range(1, int(dist.max()) + 1):
+        sel = m & (dist == r)
+        if sel.any():
+            out.append({"ring": r, "pixels": int(sel.sum()), "bias": [round(float(v), 4) for v in d[sel].mean(0)]})
+    return out
+
+
 def tonemap_f(hdr: np.ndarray) -> np.ndarray:
     """tonemap.cu:16-26 without the final truncation (float64, 8-bit units)."""
     c = np.maximum(hdr.astype(np.float64), 0.0)
@@ -87,4 +110,7 @@ def reference_pin(root, scenes, e_spp: int = 16384, spp: int = 4096) -> dict:
            "sigma": sigma, "excess_sigmas": (rho_s - rho_d) / sigma, "nan_pixels_excluded": int((m & ~finite).sum()),
            "same_stream": _agree(s8, ref, m), "disjoint": _agree(d8, ref, m)}
     out["eq_excess"] = out["same_stream"]["eq"] - out["disjoint"]["eq"]
+    out["bias_by_ring_same"] = bias_by_ring(s8, ref, m)
+    # E - ref: the same table for the noise-free expectation (8-bit units, no truncation)
+    out["bias_by_ring_expectation"] = bias_by_ring(e, ref, mc)
     return out

@@ -43,3 +43,38 @@ def test_cli_refuses_without_devices(root):
     assert r.returncode == 2, (r.returncode, r.stdout, r.stderr)
     assert "visible" in r.stderr
     assert r.stdout.strip() == ""
+
+
+def test_headline_is_strong_scaling_by_default():
+    # the metric is "1080p 1024spp, 1/2/4/8 MI355X": the fixed C3 image at every N
+    args = bench.parse_args([])
+    assert args.scaling == "strong" and args.config == "C3"
+    c = bench.CONFIGS[args.config]
+    assert (c["width"], c["height"], c["spp"]) == (1920, 1080, 1024)
+
+
+def test_gpus_below_one_exits_2(capsys):
+    with pytest.raises(SystemExit) as e:
+        bench.resolve_mode(0, 1, -1, visible(1))
+    assert e.value.code == 2
+    assert "bench.py:" in capsys.readouterr().err
+
+
+def test_group_mode_never_imports_torch(root):
+    # --group 1: libpt_hip.so is loaded by the device group before any secondary record runs, so
+    # no record may reach an `import torch` (two HIP runtimes in one process)
+    code = (
+        "import sys, bench\n"
+        "class R:\n"
+        "    mode = 'single'\n"
+        "    gather_ms = 0.0\n"
+        "    def step(self): return 1.0\n"
+        "e, k = bench.timed(R(), 2, 1, 0, False, use_torch=False)\n"
+        "assert k == 2.0, k\n"
+        "assert 'torch' not in sys.modules, 'torch imported'\n"
+        "print('ok')\n")
+    r = subprocess.run([sys.executable, "-c", code], capture_output=True, text=True, cwd=str(root), timeout=120)
+    assert r.returncode == 0 and r.stdout.strip() == "ok", (r.stdout, r.stderr)
+    src = (root / "bench.py").read_text()
+    # every timed() call passes the process's mode-derived flag
+    assert src.count("timed(") - 1 == src.count("use_torch)")

@@ -56,4 +56,5 @@ def test_pixel_pin_vs_reference_png(gpu_available, scenes, root):
     assert r["rho_same"] - r["rho_disjoint"] > 10.0 * r["sigma"], r
     assert r["eq_excess"] >= 0.2, r                          # measured 0.367 (57.8 % vs 21.2 %)
     assert s["eq"] >= 0.5 and s["le1"] >= 0.75 and s["le2"] >= 0.9 and s["le4"] >= 0.97, r
-    assert max(abs(b) for b in s["bias"]) < 1.0, r           # < 1 LSB mean difference
+    assert r["rho_same"] >= 0.95, r                          # measured 0.984
+    assert max(abs(b) for b in s["bias"]) < 0.6, r           # measured +0.45 / +0.38 / +0.32 LSB

@@ -29,7 +29,7 @@ def assert_bitexact(gpu, ref, what):
                          f"ref={ref[y, x]}; max L2 {e.max():.3g}, pixels > 1e-4: {(e > 1e-4).mean():.2%}")
 
 
-SHIPPED_VARIANTS = (1, 4, 6, 20, 39, 40, 41, 46, 47, 48, 50, 51)
+SHIPPED_VARIANTS = (1, 4, 6, 20, 39, 40, 41, 46, 47, 48)
 
 
 def pair(scene_path, W, H, row_offset=0, row_stride=1, band_rows=1):
@@ -91,31 +91,11 @@ def test_persistent_variants_large_grid(gpu_available, scenes):
     pt.set_kernel_variant(1)
     pt.render(cam, 3, True, chunks=3)
     want = pt.accum().view(np.uint32).copy()       # bits: the reference's NaN pixels stay NaN
-    for variant in (39, 40, 41, 46, 47, 48, 50, 51):
+    for variant in (39, 40, 41, 46, 47, 48):
         pt.set_kernel_variant(variant)
         pt.set_rng_state(st)
         pt.render(cam, 3, True, chunks=3)
         assert np.array_equal(pt.accum().view(np.uint32), want), f"variant {variant}"
-
-
-def test_leaf_compaction_bitexact_and_counted(gpu_available, scenes):
-    # variant 50 moves leaf tests across lanes (ds_bpermute) and accepts them back in primitive
-    # order: plain and instrumented launches give the in-order kernel's bits on the shape scene
-    # (every family, textures) and on the 484-object scene (rounds of one and two batches, and the
-    # in-order fallback), and the instrumented one counts as many primitive tests
-    for name, W, H in (("test_shapes", 96, 64), ("generated_scene", 640, 360)):
-        pt = pa.Pathtracer(W, H)
-        cam = pt.load_scene(scenes / f"{name}.scene.json")
-        st = pt.rng_state()
-        pt.set_kernel_variant(40)
-        s40 = pt.render_instrumented(cam, 4, 2, True)
-        want = pt.accum().view(np.uint32).copy()
-        for instrumented in (False, True):
-            pt.set_kernel_variant(50)
-            pt.set_rng_state(st)
-            s50 = pt.render_instrumented(cam, 4, 2, True) if instrumented else (pt.render_raw(cam, 4, 2, True), None)[1]
-            assert np.array_equal(pt.accum().view(np.uint32), want), f"{name} variant 50 instrumented={instrumented}"
-        assert s50["prim_tests"] == s40["prim_tests"] and s50["leaf_rounds"] == s40["leaf_rounds"]
 
 
 @pytest.mark.parametrize("nprims", [484, 200])
