@@ -190,7 +190,7 @@ PT_API uint32_t pt_local_rows(const pt_context *ctx);
 PT_API int pt_read_tile_costs(pt_context *ctx, uint32_t *dst, uint32_t count);
 
 /* Tuning knob for A/B measurements: 0 = automatic (default); otherwise one of the shipped
- * trace-kernel variants 1, 4, 6, 20, 39, 40, 41, 46, 47, 48 (traversal loop shape, deferred shading,
+ * trace-kernel variants 1, 4, 6, 20, 39, 40, 41, 46, 47, 48, 59, 60, 61, 66, 67 (traversal loop shape, deferred shading,
  * BVH staged in LDS or read through the caches, occupancy target; see pt_kernels.hip).  All variants
  * produce bit-identical results.  Other numbers return PT_ERR_ARG. */
 PT_API int pt_set_kernel_variant(pt_context *ctx, int variant);

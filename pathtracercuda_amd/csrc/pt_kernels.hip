@@ -75,6 +75,8 @@ struct TraceParams {
     uint32_t nodeCount, primCount, stackDepth, slabFast;
     const float4* cnodes;       // child-box records (4 per interior node), see traverse_cb
     uint32_t cnodeCount, rootWord;
+    const float4* qnodes;       // 4-wide child-box records (8 per even-depth interior node), see walk_interior_quad
+    uint32_t qnodeCount, qrootWord;
     float rootBox[6];           // (min.x, max.x, min.y, max.y, min.z, max.z) of the root
     const uint32_t* order;      // tile dispatch order as packed tile coordinates (tileY << 16 | tileX),
                                 // see "Tile scheduling"; null only with scatterWaves
@@ -594,11 +596,9 @@ struct ChildPair {
 };
 
 template <bool ALLFAST = false>
-PT_DEV ChildPair cb_children(const float4* __restrict__ cnodes, uint32_t cur, const SlabRay& R, uint32_t negMask,
-                             float tMin, float tMax)
+PT_DEV ChildPair cb_pair(const float4& Q0, const float4& Q1, const float4& Q2, const float4& Q3, const SlabRay& R,
+                         uint32_t negMask, float tMin, float tMax)
 {
-    const float4 Q0 = cnodes[4 * cur], Q1 = cnodes[4 * cur + 1];
-    const float4 Q2 = cnodes[4 * cur + 2], Q3 = cnodes[4 * cur + 3];
     float XL, XR;
     const float loL = slab_lo_x<ALLFAST>(R, f2(Q0.x, Q0.y), f2(Q0.z, Q0.w), f2(Q1.x, Q1.y), tMin, XL);
     const float loR = slab_lo_x<ALLFAST>(R, f2(Q2.x, Q2.y), f2(Q2.z, Q2.w), f2(Q1.z, Q1.w), tMin, XR);
@@ -615,6 +615,14 @@ PT_DEV ChildPair cb_children(const float4* __restrict__ cnodes, uint32_t cur, co
     c.wF = isNeg ? wL : wR;
     c.loF = isNeg ? loL : loR;
     return c;
+}
+
+template <bool ALLFAST = false>
+PT_DEV ChildPair cb_children(const float4* __restrict__ cnodes, uint32_t cur, const SlabRay& R, uint32_t negMask,
+                             float tMin, float tMax)
+{
+    return cb_pair<ALLFAST>(cnodes[4 * cur], cnodes[4 * cur + 1], cnodes[4 * cur + 2], cnodes[4 * cur + 3], R, negMask,
+                            tMin, tMax);
 }
 
 // The interior walk of the resumable traversal (trace.cu:66-77 per visited node): descend until a
@@ -635,6 +643,80 @@ PT_DEV bool walk_interior(const float4* __restrict__ cnodes, uint2* stack, const
         sp += ch.both ? 1u : 0u;
         if (ch.any) {
             cur = ch.wNext;
+        } else {
+            bool found = false;
+            while (sp > 0) {
+                const uint2 e = stack[64u * (--sp)];
+                if (tMax > __uint_as_float(e.y)) { cur = e.x; found = true; break; }
+            }
+            if (!found) return true;
+        }
+    }
+    return false;
+}
+
+// ---------------------------------------------------------------------------------------------
+// 4-wide child-box traversal (QUAD).  Device layout "qnodes": one 128-byte record per interior node
+// at EVEN depth of the reference BVH (a "landing" node N; root = depth 0), two halves of the
+// child-box format above:
+//   half 0 = N's first child A = N + 1:  A interior -> A's two children (A + 1, A.offset) with their
+//            boxes and words and 1 << A's split axis; A a leaf -> slot L = A itself, slot R empty
+//   half 1 = N's second child B = N.offset, the same;   half 0's Q3.w = 1 << N's split axis.
+// A child word is (count << 24 | prim offset) for a leaf, the record index of an even-depth
+// interior node, or a PAIR reference (1 << 23 | 2 r + h): "half h of record r" -- the odd-depth
+// node whose two children that half holds.  An empty slot has the box [+inf, +inf]^3, which no ray
+// hits in either slab form.
+//
+// A landing visit tests the four grandchild boxes (or the leaf children) at once, with one 128-byte
+// fetch, instead of visiting N and then its near child with two dependent fetches.  Exactness: the
+// slab test of a child box nested in its parent's (host-checked: min >= parent min, max <= parent
+// max, no NaN) can only pass if the parent's passes -- per axis the child's slab interval lies
+// inside the parent's, in float arithmetic too (subtraction and multiplication round
+// monotonically; an infinite 1/d gives both boxes the same +-inf or no-constraint NaN bound) -- so
+// testing the near child's children directly gives the reference's verdicts (trace.cu:48-77: near
+// child tested at the same t_max, then its children at the same t_max).  The far side is pushed as
+// ONE entry, as the reference pushes the far child (trace.cu:75): if both of its children hit now,
+// a PAIR reference with lo = the smaller of their entry distances -- when popped with t_max <= lo
+// neither child can pass (t_max only falls), otherwise the pair is visited and both children are
+// re-tested with the then-current t_max, exactly the reference's visit of the far child (its own
+// box test implied by nesting); if one child hits, that child's word and lo, as a plain far entry;
+// if none, nothing (it fails at any later, smaller t_max).  A pair visit fetches the same record
+// and enables only its half.  Visit order, node culling and primitive tests per lane are the
+// reference's; the stack holds at most the reference's pending count (<= one entry per level).
+// ---------------------------------------------------------------------------------------------
+constexpr uint32_t kPairBit = 1u << 23;
+
+template <bool STATS, bool ALLFAST>
+PT_DEV bool walk_interior_quad(const float4* __restrict__ qnodes, uint2* stack, const SlabRay& R, uint32_t negMask,
+                               float tMin, float tMax, uint32_t& cur, uint32_t& sp, Counters& cnt)
+{
+    while ((cur >> 24) == 0u) {
+        if (STATS) { cnt.node_tests += 4; wave_tick(cnt.w_node); }
+        const bool isPair = (cur & kPairBit) != 0u;
+        const uint32_t r = isPair ? (cur & (kPairBit - 1u)) >> 1 : cur;
+        const float4* q = qnodes + 8 * r;
+        const float4 A0 = q[0], A1 = q[1], A2 = q[2], A3 = q[3];
+        const float4 B0 = q[4], B1 = q[5], B2 = q[6], B3 = q[7];
+        const ChildPair hA = cb_pair<ALLFAST>(A0, A1, A2, A3, R, negMask, tMin, tMax);
+        const ChildPair hB = cb_pair<ALLFAST>(B0, B1, B2, B3, R, negMask, tMin, tMax);
+        // near side: by N's split axis on a landing visit (trace.cu:69-76), the referenced half on a pair visit
+        const bool nearIsB = isPair ? (cur & 1u) != 0u : (negMask & __float_as_uint(A3.w)) != 0u;
+        const ChildPair& nr = nearIsB ? hB : hA;
+        const ChildPair& fr = nearIsB ? hA : hB;
+        const bool farOn = !isPair && fr.any;
+        // descend into the near side if any of its children passes, else into the far side (same t_max)
+        const bool intoNear = nr.any;
+        const ChildPair& sd = intoNear ? nr : fr;
+        // entry 1: the far side, below the near side's far child (pushed only when descending near)
+        const uint32_t w1 = fr.both ? (kPairBit | (2u * r + (nearIsB ? 0u : 1u))) : fr.wNext;
+        const float lo1 = fr.both ? __builtin_fminf(fr.loNext, fr.loF) : fr.loNext;
+        stack[64u * sp] = make_uint2(w1, __float_as_uint(lo1));
+        sp += (intoNear && farOn) ? 1u : 0u;
+        // entry 2: the far child of the side descended into
+        stack[64u * sp] = make_uint2(sd.wF, __float_as_uint(sd.loF));
+        sp += sd.both ? 1u : 0u;
+        if (intoNear || farOn) {
+            cur = sd.wNext;
         } else {
             bool found = false;
             while (sp > 0) {
@@ -732,7 +814,7 @@ struct TravState {
 
 // The interior walk is walk_interior (the lean form: wave-uniform slab-form choice, unconditional
 // far-child write).  WW = 200 + EXITQ selects this traversal.
-template <bool STATS, int EXITQ>
+template <bool STATS, int EXITQ, bool QUAD = false>
 PT_DEV bool traverse_cb_phase(const float4* __restrict__ cnodes, const float4* __restrict__ prims, uint2* stack,
                               const TraceParams& P, f3 o, f3 d, bool fresh, TravState& ts, Counters& cnt)
 {
@@ -756,7 +838,7 @@ PT_DEV bool traverse_cb_phase(const float4* __restrict__ cnodes, const float4* _
         ts.tMax = kFltMax;
         ts.sp = 0;
         ts.elem = 0xffffffffu;
-        ts.cur = P.rootWord;
+        ts.cur = QUAD ? P.qrootWord : P.rootWord;
         if (STATS) { cnt.node_tests++; wave_tick(cnt.w_node); }
         float X;
         const float lo0 = slab_lo_x(R, f2(P.rootBox[0], P.rootBox[1]), f2(P.rootBox[2], P.rootBox[3]),
@@ -775,8 +857,12 @@ PT_DEV bool traverse_cb_phase(const float4* __restrict__ cnodes, const float4* _
     uint64_t tPhase = STATS ? __builtin_amdgcn_s_memtime() : 0;
     const bool allFast = __ballot(!R.fast) == 0;                         // wave-uniform
     while (!done) {
-        done = allFast ? walk_interior<STATS, true>(cnodes, stack, R, negMask, tMin, tMax, cur, sp, cnt)
-                       : walk_interior<STATS, false>(cnodes, stack, R, negMask, tMin, tMax, cur, sp, cnt);
+        if (QUAD)
+            done = allFast ? walk_interior_quad<STATS, true>(cnodes, stack, R, negMask, tMin, tMax, cur, sp, cnt)
+                           : walk_interior_quad<STATS, false>(cnodes, stack, R, negMask, tMin, tMax, cur, sp, cnt);
+        else
+            done = allFast ? walk_interior<STATS, true>(cnodes, stack, R, negMask, tMin, tMax, cur, sp, cnt)
+                           : walk_interior<STATS, false>(cnodes, stack, R, negMask, tMin, tMax, cur, sp, cnt);
         if (STATS) wave_time(cnt.cyc_node, tPhase);
         if (done) break;
         uint32_t leafOff = cur & 0xffffffu, leafCnt = cur >> 24;
@@ -1388,8 +1474,12 @@ __global__ void __launch_bounds__(WPB * 64, MINW) trace_kernel(TraceParams P)
     constexpr bool SSG = MODE == 1, AUX = MODE == 2;
     const uint32_t lane = threadIdx.x & 63u;
     const uint32_t wave = threadIdx.x >> 6;
-    const float4* gnodes = WW >= 3 ? P.cnodes : P.nodes;
-    const uint32_t nodeF4 = WW >= 3 ? 4u * P.cnodeCount : 2u * P.nodeCount;
+    // QUAD (WW / 100000 == 1): the 4-wide child-box walk over qnodes (walk_interior_quad), whose
+    // unconditional stack writes reach one slot above the reference's pending count
+    constexpr bool QUAD = WW >= 100 && (WW / 100000) % 10 == 1;
+    const float4* gnodes = QUAD ? P.qnodes : (WW >= 3 ? P.cnodes : P.nodes);
+    const uint32_t nodeF4 = QUAD ? 8u * P.qnodeCount : (WW >= 3 ? 4u * P.cnodeCount : 2u * P.nodeCount);
+    const uint32_t stackDepth = P.stackDepth + (QUAD ? 1u : 0u);
     const uint32_t sceneF4 = (SL >= 1 ? nodeF4 : 0u) + (SL >= 2 ? 4u * P.primCount : 0u);
     if (SL >= 1) {
         for (uint32_t i = threadIdx.x; i < nodeF4; i += WPB * 64) lds4[i] = gnodes[i];
@@ -1402,7 +1492,7 @@ __global__ void __launch_bounds__(WPB * 64, MINW) trace_kernel(TraceParams P)
     // wave stacks: stackDepth x 64 entries of u32 (node index), or of uint2 (word, lo) for WW >= 3;
     // then one accumulation slice per wave (3 planes of 64 floats)
     uint32_t* ldsStacks = reinterpret_cast<uint32_t*>(lds4 + sceneF4);
-    const uint32_t stackWords = (WW >= 3 ? 2u : 1u) * P.stackDepth * 64u;
+    const uint32_t stackWords = (WW >= 3 ? 2u : 1u) * stackDepth * 64u;
     uint32_t* stack = ldsStacks + wave * stackWords + (WW >= 3 ? 2u : 1u) * lane;
     const uint32_t accL = 4u * sceneF4 + WPB * stackWords + wave * 192u + lane;   // float index
     Counters cnt = {};
@@ -1454,7 +1544,7 @@ __global__ void __launch_bounds__(WPB * 64, MINW) trace_kernel(TraceParams P)
                 if (STATS && fresh && !held) { cnt.segments++; wave_tick(cnt.w_segments); }
                 bool tdone = true;
                 if (!held) {
-                    tdone = traverse_cb_phase<STATS, WW % 100>(nodes, prims, reinterpret_cast<uint2*>(stack), P,
+                    tdone = traverse_cb_phase<STATS, WW % 100, QUAD>(nodes, prims, reinterpret_cast<uint2*>(stack), P,
                                                                 ps.o, ps.d, fresh, ts, cnt);
                     fresh = tdone;
                 }
@@ -1905,6 +1995,8 @@ struct pt_context {
     float4* mats = nullptr;
     float4* cnodes = nullptr;   // child-box records (traverse_cb); null when the scene exceeds its encoding
     uint32_t cnodeCount = 0, rootWord = 0;
+    float4* qnodes = nullptr;   // 4-wide child-box records (walk_interior_quad); null when boxes are not nested
+    uint32_t qnodeCount = 0, qrootWord = 0;
     float rootBox[6] = {};
     uint32_t nodeCount = 0, primCount = 0, stackDepth = 1;
     bool slabFast = true;
@@ -1988,9 +2080,12 @@ static int fail(pt_context* ctx, int code, const char* msg)
 template <bool STATS, int SL, int WPB, int WW, int MINW, bool PERSIST = false, int MODE = 0>
 static hipError_t launch_one(const TraceParams& P, hipStream_t stream)
 {
-    const size_t nodeF4 = WW >= 3 ? 4 * (size_t)P.cnodeCount : 2 * (size_t)P.nodeCount;
+    constexpr bool QUAD = WW >= 100 && (WW / 100000) % 10 == 1;
+    if (QUAD && P.qnodes == nullptr)           // no 4-wide layout (unnested boxes): the 2-wide walk
+        return launch_one<STATS, SL, WPB, WW % 100000, MINW, PERSIST, MODE>(P, stream);
+    const size_t nodeF4 = QUAD ? 8 * (size_t)P.qnodeCount : (WW >= 3 ? 4 * (size_t)P.cnodeCount : 2 * (size_t)P.nodeCount);
     const size_t sceneBytes = ((SL >= 1 ? nodeF4 : 0) + (SL >= 2 ? 4 * (size_t)P.primCount : 0)) * sizeof(float4);
-    const size_t lds = sceneBytes + (size_t)WPB * P.stackDepth * 64 * (WW >= 3 ? 8 : 4) + (size_t)WPB * 64 * 12;
+    const size_t lds = sceneBytes + (size_t)WPB * (P.stackDepth + (QUAD ? 1 : 0)) * 64 * (WW >= 3 ? 8 : 4) + (size_t)WPB * 64 * 12;
     if (WW >= 3 && P.cnodes == nullptr) return MODE == 1 ? hipErrorInvalidValue : launch_one<STATS, SL, WPB, 1, MINW, PERSIST, MODE>(P, stream);  // no child-box layout
     if (lds > 160 * 1024) {
         // scene too large to stage in LDS: the same variant reading the scene through the caches
@@ -2076,6 +2171,11 @@ static hipError_t launch_variant(int v, const TraceParams& P, hipStream_t stream
     case 46: return launch_one<STATS, 0, 4, 14212, 4, true, MODE>(P, stream);
     case 47: return launch_one<STATS, 1, 4, 224, 4, true, MODE>(P, stream);
     case 48: return launch_one<STATS, 2, 4, 13216, 4, true, MODE>(P, stream);
+    case 59: return launch_one<STATS, 1, 4, 100000 + 224, 5, true, MODE>(P, stream);
+    case 60: return launch_one<STATS, 1, 4, 100000 + kV40Walk, 5, true, MODE>(P, stream);
+    case 61: return launch_one<STATS, 0, 4, 100000 + 14212, 5, true, MODE>(P, stream);
+    case 66: return launch_one<STATS, 0, 4, 100000 + 14212, 4, true, MODE>(P, stream);
+    case 67: return launch_one<STATS, 1, 4, 100000 + 224, 4, true, MODE>(P, stream);
     default: return hipErrorInvalidValue;
     }
 }
@@ -2090,13 +2190,18 @@ static hipError_t launch_grouped(int v, const TraceParams& P, hipStream_t stream
     case 40: return launch_one<false, 1, 4, kV40Walk, 5, true, MODE>(P, stream);
     case 41: return launch_one<false, 0, 4, 14212, 5, true, MODE>(P, stream);
     case 46: return launch_one<false, 0, 4, 14212, 4, true, MODE>(P, stream);
+    case 59: return launch_one<false, 1, 4, 100000 + 224, 5, true, MODE>(P, stream);
+    case 60: return launch_one<false, 1, 4, 100000 + kV40Walk, 5, true, MODE>(P, stream);
+    case 61: return launch_one<false, 0, 4, 100000 + 14212, 5, true, MODE>(P, stream);
+    case 66: return launch_one<false, 0, 4, 100000 + 14212, 4, true, MODE>(P, stream);
     default: return hipErrorInvalidValue;
     }
 }
 
 static bool variant_shipped(int v)
 {
-    return v == 0 || v == 1 || v == 4 || v == 6 || v == 20 || v == 40 || v == 41 || v == 46 || v == 47 || v == 48 || v == 39;
+    return v == 0 || v == 1 || v == 4 || v == 6 || v == 20 || v == 40 || v == 41 || v == 46 || v == 47 || v == 48 || v == 39 ||
+           v == 59 || v == 60 || v == 61 || v == 66 || v == 67;
 }
 
 // Cost pre-pass of a cold-start launch (render_impl): samples per pixel, and the smallest launch
@@ -2210,6 +2315,7 @@ PT_API void pt_destroy(pt_context* ctx)
     (void)hipFree(ctx->prims);
     (void)hipFree(ctx->mats);
     (void)hipFree(ctx->cnodes);
+    (void)hipFree(ctx->qnodes);
     (void)hipFree(ctx->tileCost);
     (void)hipFree(ctx->order);
     (void)hipFree(ctx->rowMajor);
@@ -2316,6 +2422,54 @@ PT_API int pt_set_scene(pt_context* ctx, const pt_bvh_node* nodes, uint32_t node
         q[2] = make_float4(R.aabb_min[0], R.aabb_max[0], R.aabb_min[1], R.aabb_max[1]);
         q[3] = make_float4(u2f(word(i + 1)), u2f(word(nodes[i].offset)), u2f(1u << ((nodes[i].primitive_count_axis >> 8) & 0xffu)), 0.0f);
     }
+    // 4-wide records (walk_interior_quad): interior nodes at even depth, in node order; every child
+    // box must lie inside its parent's (the exactness argument), else the 2-wide walk is used
+    std::vector<uint32_t> qrec(node_count, 0xffffffffu);
+    uint32_t quads = 0;
+    bool qOk = cbOk;
+    {
+        std::vector<uint8_t> depthOdd(node_count, 0);
+        for (uint32_t i = 0; qOk && i < node_count; ++i) {
+            if ((nodes[i].primitive_count_axis >> 16) != 0) continue;
+            for (const uint32_t c : {i + 1, nodes[i].offset}) {
+                depthOdd[c] = depthOdd[i] ^ 1u;            // parents precede children (validate_scene)
+                for (int k = 0; k < 3; ++k)
+                    if (!(nodes[c].aabb_min[k] >= nodes[i].aabb_min[k] && nodes[c].aabb_max[k] <= nodes[i].aabb_max[k]))
+                        qOk = false;
+            }
+            if (!depthOdd[i]) qrec[i] = quads++;
+        }
+        qOk = qOk && quads < (1u << 22);
+    }
+    auto qword = [&](uint32_t i) {
+        const uint32_t count = nodes[i].primitive_count_axis >> 16;
+        return count ? (count << 24) | nodes[i].offset : qrec[i];
+    };
+    const float kInf = __builtin_inff();
+    std::vector<float4> hq(qOk ? 8 * (size_t)std::max(quads, 1u) : 0, make_float4(kInf, kInf, kInf, kInf));
+    for (uint32_t i = 0; qOk && i < node_count; ++i) {
+        if (qrec[i] == 0xffffffffu) continue;
+        float4* q = &hq[8 * (size_t)qrec[i]];
+        const uint32_t side[2] = {i + 1, nodes[i].offset};
+        for (int h = 0; h < 2; ++h, q += 4) {
+            const uint32_t c = side[h];
+            const bool leaf = (nodes[c].primitive_count_axis >> 16) != 0;
+            const pt_bvh_node& L = leaf ? nodes[c] : nodes[c + 1];
+            q[0] = make_float4(L.aabb_min[0], L.aabb_max[0], L.aabb_min[1], L.aabb_max[1]);
+            q[1] = make_float4(L.aabb_min[2], L.aabb_max[2], kInf, kInf);       // slot R empty for a leaf side
+            uint32_t wR = 0xffffffffu, axisBit = 0;
+            if (!leaf) {
+                const pt_bvh_node& R = nodes[nodes[c].offset];
+                q[1].z = R.aabb_min[2];
+                q[1].w = R.aabb_max[2];
+                q[2] = make_float4(R.aabb_min[0], R.aabb_max[0], R.aabb_min[1], R.aabb_max[1]);
+                wR = qword(nodes[c].offset);
+                axisBit = 1u << ((nodes[c].primitive_count_axis >> 8) & 0xffu);
+            }
+            const uint32_t axisN = h == 0 ? 1u << ((nodes[i].primitive_count_axis >> 8) & 0xffu) : 0u;
+            q[3] = make_float4(u2f(leaf ? qword(c) : qword(c + 1)), u2f(wR), u2f(axisBit), u2f(axisN));
+        }
+    }
     for (uint32_t i = 0; i < prim_count; ++i) {
         const pt_hittable& h = prims[i];
         const float(&R)[3][4] = h.inv_transform_rows;
@@ -2333,8 +2487,9 @@ PT_API int pt_set_scene(pt_context* ctx, const pt_bvh_node* nodes, uint32_t node
     (void)hipFree(ctx->prims);
     (void)hipFree(ctx->mats);
     (void)hipFree(ctx->cnodes);
-    ctx->nodes = ctx->prims = ctx->mats = ctx->cnodes = nullptr;
-    ctx->nodeCount = ctx->primCount = ctx->cnodeCount = 0;
+    (void)hipFree(ctx->qnodes);
+    ctx->nodes = ctx->prims = ctx->mats = ctx->cnodes = ctx->qnodes = nullptr;
+    ctx->nodeCount = ctx->primCount = ctx->cnodeCount = ctx->qnodeCount = 0;
     PT_HIP_CHECK(ctx, hipMalloc(&ctx->nodes, hn.size() * sizeof(float4)));
     PT_HIP_CHECK(ctx, hipMalloc(&ctx->prims, hp.size() * sizeof(float4)));
     PT_HIP_CHECK(ctx, hipMalloc(&ctx->mats, hm.size() * sizeof(float4)));
@@ -2345,6 +2500,12 @@ PT_API int pt_set_scene(pt_context* ctx, const pt_bvh_node* nodes, uint32_t node
         PT_HIP_CHECK(ctx, hipMalloc(&ctx->cnodes, hc.size() * sizeof(float4)));
         PT_HIP_CHECK(ctx, hipMemcpy(ctx->cnodes, hc.data(), hc.size() * sizeof(float4), hipMemcpyHostToDevice));
         ctx->cnodeCount = interior;
+    }
+    if (qOk) {
+        PT_HIP_CHECK(ctx, hipMalloc(&ctx->qnodes, hq.size() * sizeof(float4)));
+        PT_HIP_CHECK(ctx, hipMemcpy(ctx->qnodes, hq.data(), hq.size() * sizeof(float4), hipMemcpyHostToDevice));
+        ctx->qnodeCount = quads;
+        ctx->qrootWord = qword(0);
     }
     ctx->orderStale = true;
     ctx->rootWord = word(0);
@@ -2652,6 +2813,9 @@ static int render_impl(pt_context* ctx, const pt_camera* cam, uint32_t spp, uint
     P.cnodes = ctx->cnodes;
     P.cnodeCount = ctx->cnodeCount;
     P.rootWord = ctx->rootWord;
+    P.qnodes = ctx->qnodes;
+    P.qnodeCount = ctx->qnodeCount;
+    P.qrootWord = ctx->qrootWord;
     for (int k = 0; k < 6; ++k) P.rootBox[k] = ctx->rootBox[k];
     // Tile scheduling: a pixel's samples are sequential (one XORWOW stream), so a tile is the
     // smallest unit of work, and tiles differ several-fold in cost (sky vs geometry).  Every

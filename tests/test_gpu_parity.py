@@ -29,7 +29,7 @@ def assert_bitexact(gpu, ref, what):
                          f"ref={ref[y, x]}; max L2 {e.max():.3g}, pixels > 1e-4: {(e > 1e-4).mean():.2%}")
 
 
-SHIPPED_VARIANTS = (1, 4, 6, 20, 39, 40, 41, 46, 47, 48)
+SHIPPED_VARIANTS = (1, 4, 6, 20, 39, 40, 41, 46, 47, 48, 59, 60, 61, 66, 67)
 
 
 def pair(scene_path, W, H, row_offset=0, row_stride=1, band_rows=1):
@@ -91,7 +91,7 @@ def test_persistent_variants_large_grid(gpu_available, scenes):
     pt.set_kernel_variant(1)
     pt.render(cam, 3, True, chunks=3)
     want = pt.accum().view(np.uint32).copy()       # bits: the reference's NaN pixels stay NaN
-    for variant in (39, 40, 41, 46, 47, 48):
+    for variant in (39, 40, 41, 46, 47, 48, 59, 60, 61, 66, 67):
         pt.set_kernel_variant(variant)
         pt.set_rng_state(st)
         pt.render(cam, 3, True, chunks=3)

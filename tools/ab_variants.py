@@ -28,6 +28,9 @@ def main():
     ap.add_argument("--rank", type=int, default=0)
     ap.add_argument("--groups", type=int, default=1, help="sample groups: 1 = off (plain launches), 0 = automatic")
     a = ap.parse_args()
+    if a.scene == "stress_100k":                   # C5's generated scene (bench.scene_path)
+        import bench
+        a.scene = bench.scene_path("stress_100k")
     vs = [(int(v), int(m)) for v in a.variants.split(",") for m in a.schedules.split(",")]
     pt = (pa.Pathtracer(a.width, a.height, row_offset=a.rank, row_stride=a.n, band_rows=8) if a.n > 1
           else pa.Pathtracer(a.width, a.height))

@@ -19,6 +19,9 @@ ap.add_argument("--variants", default="40")
 ap.add_argument("--spp", type=int, default=8)
 ap.add_argument("--chunks", type=int, default=1)
 a = ap.parse_args()
+if a.scene == "stress_100k":                       # C5's generated scene (bench.scene_path)
+    import bench  # noqa: E402
+    a.scene = bench.scene_path("stress_100k")
 pt = pa.Pathtracer(a.width, a.height)
 cam = pt.load_scene(a.scene)
 res = {}
