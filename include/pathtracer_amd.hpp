@@ -249,7 +249,7 @@ struct Params {
     bool m_outputHdr = false;
     // additions
     unsigned int m_chunk = 8;        // samples per render() call of the headless loop (main.cpp:272)
-    bool m_singleLaunch = false;     // run all chunks in one launch (bit-identical)
+    bool m_singleLaunch = true;      // run all chunks in one launch (bit-identical; CLI -call_loop: false)
 };
 
 Camera loadScene(Pathtracer& pathtracer, const Params& params);

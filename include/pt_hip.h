@@ -188,6 +188,11 @@ PT_API uint32_t pt_local_rows(const pt_context *ctx);
 /* Shader-clock cycles each 8x8 tile took in the last launch (row-major over the context's tiles,
  * count = ceil(width / 8) * ceil(rows / 8)); the input of the cost order. */
 PT_API int pt_read_tile_costs(pt_context *ctx, uint32_t *dst, uint32_t count);
+/* Diagnostics: per tile (row-major, same count), the mean over its lanes of the shader-clock cycles
+ * between a lane finishing its pixel and the tile's end, from the last pt_render_instrumented launch
+ * (resumable variants).  Divided by the tile's cycles (pt_read_tile_costs) it is the tile's
+ * idle-lane fraction. */
+PT_API int pt_read_tile_idle(pt_context *ctx, uint32_t *dst, uint32_t count);
 
 /* Tuning knob for A/B measurements: 0 = automatic (default); otherwise one of the shipped
  * trace-kernel variants 1, 4, 6, 20, 39, 40, 41, 46, 47, 48, 59, 60, 61, 66, 67 (traversal loop shape, deferred shading,

@@ -367,6 +367,15 @@ class Pathtracer:
         N.check_ctx(N.hip().pt_read_tile_costs(self._ctx, out.ctypes.data_as(C.POINTER(C.c_uint32)), tx * ty), self._ctx)
         return out.reshape(ty, tx)
 
+    def tile_idle(self) -> np.ndarray:
+        """Per tile of the last instrumented launch: mean lane cycles spent done while the tile ran
+        (tiles_y x tiles_x; divide by tile_costs() for the idle-lane fraction)."""
+        self._single("tile_idle")
+        tx, ty = (self.width + 7) // 8, (self.rows + 7) // 8
+        out = np.zeros(tx * ty, dtype=np.uint32)
+        N.check_ctx(N.hip().pt_read_tile_idle(self._ctx, out.ctypes.data_as(C.POINTER(C.c_uint32)), tx * ty), self._ctx)
+        return out.reshape(ty, tx)
+
     def copy_accum_to_device(self, dst_ptr: int, nbytes: int) -> None:
         self._single("copy_accum_to_device")
         N.check_ctx(N.hip().pt_copy_accum_device(self._ctx, C.c_void_p(int(dst_ptr)), int(nbytes)), self._ctx)

@@ -84,6 +84,8 @@ struct TraceParams {
     uint32_t* tileCursor;       // persistent variants: {next dispatch slot, waves finished}, rewound by the last wave
     uint32_t numSlots;          // dispatch slots = 8x8 tiles
     uint32_t* tileCost;         // per-tile shader-clock cycles of this launch (null: not recorded)
+    uint32_t* tileIdle;         // instrumented launches: per tile, the lanes' mean cycles between finishing
+                                // their pixel and the tile's end (zeroed before the launch)
     uint32_t discard;           // != 0: cost pre-pass -- pixel state (RNG, accum) is read, never written
     float* pairsOut;            // cost pre-pass: per-pixel draw pairs per sample (speculative groups' guess)
     // Speculative sample groups (0 = off).  A tile has J = 2G - 1 work items: item 0 =
@@ -1581,7 +1583,12 @@ __global__ void __launch_bounds__(WPB * 64, MINW) trace_kernel(TraceParams P)
             }
             if (STATS) wave_time(cnt.cyc_shade, tS);
         }
-        if (STATS && WW >= 100 && tDone) cnt.cyc_lane_idle += __builtin_amdgcn_s_memtime() - tDone;
+        if (STATS && WW >= 100 && tDone) {
+            const uint64_t idle = __builtin_amdgcn_s_memtime() - tDone;
+            cnt.cyc_lane_idle += idle;
+            if (P.tileIdle && (tile >> 16) < P.tilesY)
+                atomicAdd(&P.tileIdle[(tile >> 16) * P.tilesX + (tile & 0xffffu)], (uint32_t)min(idle >> 6, (uint64_t)0x3ffffffu));
+        }
         if (STATS) wave_time(cnt.cyc_total, tAll);
         if (SSG) P.ssgCount[(size_t)sl.logItem * 64 + lane] = sl.k;
         else if (!P.discard) store_pixel(P, pc, rng, ps);
@@ -2007,6 +2014,7 @@ struct pt_context {
     unsigned long long* stats = nullptr;
     // tile scheduling: per-tile cost of the last launch and the cost-sorted dispatch order
     uint32_t* tileCost = nullptr;
+    uint32_t* tileIdle = nullptr;     // instrumented launches: per-tile mean lane idle cycles (pt_read_tile_idle)
     uint32_t* order = nullptr;
     uint32_t* rowMajor = nullptr;     // the row-major order (packed coordinates), before costs are known
     uint32_t* tileCursor = nullptr;   // persistent variants
@@ -2317,6 +2325,7 @@ PT_API void pt_destroy(pt_context* ctx)
     (void)hipFree(ctx->cnodes);
     (void)hipFree(ctx->qnodes);
     (void)hipFree(ctx->tileCost);
+    (void)hipFree(ctx->tileIdle);
     (void)hipFree(ctx->order);
     (void)hipFree(ctx->rowMajor);
     (void)hipFree(ctx->tileCursor);
@@ -2830,8 +2839,10 @@ static int render_impl(pt_context* ctx, const pt_camera* cam, uint32_t spp, uint
     if (ctx->orderTiles != tiles) {
         (void)hipFree(ctx->tileCost);
         (void)hipFree(ctx->order);
+        (void)hipFree(ctx->tileIdle);
         ctx->tileCost = nullptr;
         ctx->order = nullptr;
+        ctx->tileIdle = nullptr;
         ctx->orderTiles = 0;
         ctx->orderValid = false;
         PT_HIP_CHECK(ctx, hipMalloc(&ctx->tileCost, (size_t)tiles * sizeof(uint32_t)));
@@ -2886,7 +2897,12 @@ static int render_impl(pt_context* ctx, const pt_camera* cam, uint32_t spp, uint
     const bool rebuilds = ctx->schedule == 0 &&
                           (ctx->orderStale || !ctx->orderValid || (uint64_t)spp * chunks >= 4 * ctx->orderSamples);
     if (!rebuilds || ctx->prioMode == 2) issue_priority(ctx, tiles, P.prio);   // explicit bounds: always
-    if (stats) PT_HIP_CHECK(ctx, hipMemsetAsync(ctx->stats, 0, kStatWords * sizeof(unsigned long long), ctx->stream));
+    if (stats) {
+        PT_HIP_CHECK(ctx, hipMemsetAsync(ctx->stats, 0, kStatWords * sizeof(unsigned long long), ctx->stream));
+        if (!ctx->tileIdle) PT_HIP_CHECK(ctx, hipMalloc(&ctx->tileIdle, (size_t)tiles * sizeof(uint32_t)));
+        PT_HIP_CHECK(ctx, hipMemsetAsync(ctx->tileIdle, 0, (size_t)tiles * sizeof(uint32_t), ctx->stream));
+        P.tileIdle = ctx->tileIdle;
+    }
     int variant = pick_variant(ctx);
     // speculative sample groups
     const uint32_t total = spp * chunks;
@@ -3163,6 +3179,16 @@ PT_API int pt_read_tile_costs(pt_context* ctx, uint32_t* dst, uint32_t count)
     PT_HIP_CHECK(ctx, hipSetDevice(ctx->device));
     PT_HIP_CHECK(ctx, hipStreamSynchronize(ctx->stream));
     PT_HIP_CHECK(ctx, hipMemcpy(dst, ctx->tileCost, (size_t)count * sizeof(uint32_t), hipMemcpyDeviceToHost));
+    return PT_OK;
+}
+
+PT_API int pt_read_tile_idle(pt_context* ctx, uint32_t* dst, uint32_t count)
+{
+    if (!ctx || !dst) return PT_ERR_ARG;
+    if (!ctx->tileIdle || count != ctx->orderTiles) return fail(ctx, PT_ERR_STATE, "pt_read_tile_idle: no instrumented launch of that size");
+    PT_HIP_CHECK(ctx, hipSetDevice(ctx->device));
+    PT_HIP_CHECK(ctx, hipStreamSynchronize(ctx->stream));
+    PT_HIP_CHECK(ctx, hipMemcpy(dst, ctx->tileIdle, (size_t)count * sizeof(uint32_t), hipMemcpyDeviceToHost));
     return PT_OK;
 }
 

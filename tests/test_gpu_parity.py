@@ -535,14 +535,14 @@ def test_stress_100k_row_subset(gpu_available, tmp_path, root):
 
 def test_cli_headless_outputs(gpu_available, tmp_path, scenes):
     # the `pathtracer` CLI (main.cpp headless path): PNG = tonemapped image flipped vertically,
-    # -ohdr = accumulation / frames; -single_launch and -gpus 1 give the same files
+    # -ohdr = accumulation / frames; the default (one launch) and -call_loop give the same files
     import subprocess
     from pathtracercuda_amd import _native as N
     from PIL import Image
     scene = scenes / "test_shapes.scene.json"
     W, H, SPP = 64, 40, 20                       # 20 spp = render() calls of 8, 8, 4
     outs = {}
-    for tag, extra in [("loop", []), ("single", ["-single_launch"])]:
+    for tag, extra in [("loop", ["-call_loop"]), ("single", [])]:
         png = tmp_path / f"{tag}.png"
         r = subprocess.run([str(N.CLI), "-w", str(W), "-h", str(H), "-spp", str(SPP), *extra, "-o", str(png), str(scene)],
                            capture_output=True, text=True, timeout=120)
