@@ -132,6 +132,13 @@ PT_API int pt_create_banded(int device, uint32_t width, uint32_t height, uint32_
 
 /* Number of local rows of such a context (0 if it owns no band or the arguments are invalid). */
 PT_API uint32_t pt_band_rows(uint32_t height, uint32_t band_rows, uint32_t band_offset, uint32_t band_stride);
+/* Scatter one tile's rows (pt_band_rows(height, ...) x width float4, local row order, device memory
+ * `part`) into the full image (height x width float4, device memory `full`) on `device`: the
+ * unpermute step of pt_group_gather, for callers that gathered the tiles themselves (the
+ * one-process-per-GPU path over torch.distributed / RCCL, pathtracercuda_amd/distributed.py).
+ * Synchronises the device before and after. */
+PT_API int pt_unpermute_bands(int device, void *full, const void *part, uint32_t width, uint32_t height,
+                              uint32_t band_rows, uint32_t band_offset, uint32_t band_stride);
 PT_API void pt_destroy(pt_context *ctx);
 
 /* Pathtracer::setScene upload half (Pathtracer.cpp:137-159): nodes and primitives as produced by

@@ -693,7 +693,7 @@ PT_DEV bool walk_interior_quad(const float4* __restrict__ qnodes, uint2* stack, 
                                float tMin, float tMax, uint32_t& cur, uint32_t& sp, Counters& cnt)
 {
     while ((cur >> 24) == 0u) {
-        if (STATS) { cnt.node_tests += 4; wave_tick(cnt.w_node); }
+        if (STATS) { cnt.node_tests += 2; wave_tick(cnt.w_node); }   // one visit (bench.lane_utilisation)
         const bool isPair = (cur & kPairBit) != 0u;
         const uint32_t r = isPair ? (cur & (kPairBit - 1u)) >> 1 : cur;
         const float4* q = qnodes + 8 * r;
@@ -2257,6 +2257,28 @@ PT_API uint32_t pt_band_rows(uint32_t height, uint32_t band_rows, uint32_t band_
     const uint32_t own = (nb - band_offset + band_stride - 1) / band_stride;
     const uint32_t last = band_offset + (own - 1) * band_stride;
     return (own - 1) * band_rows + std::min(band_rows, height - last * band_rows);
+}
+
+PT_API int pt_unpermute_bands(int device, void* full, const void* part, uint32_t width, uint32_t height, uint32_t band_rows,
+                              uint32_t band_offset, uint32_t band_stride)
+{
+    if (!full || !part || width == 0 || band_stride == 0 || band_rows == 0 || band_rows > 256 ||
+        (band_rows & (band_rows - 1)) != 0)
+        return PT_ERR_ARG;
+    int n = 0;
+    if (hipGetDeviceCount(&n) != hipSuccess || n == 0) return PT_ERR_NO_DEVICE;
+    if (device < 0 || device >= n) return PT_ERR_ARG;
+    const uint32_t rows = pt_band_rows(height, band_rows, band_offset, band_stride);
+    const size_t npix = (size_t)rows * width;
+    if (npix == 0) return PT_OK;
+    if (hipSetDevice(device) != hipSuccess) return PT_ERR_HIP;
+    // the caller's buffers may be in use on any stream of the device: synchronise around the copy
+    if (hipDeviceSynchronize() != hipSuccess) return PT_ERR_HIP;
+    unpermute_rows_kernel<<<(unsigned)((npix + 255) / 256), 256, 0, 0>>>(
+        static_cast<float4*>(full), static_cast<const float4*>(part), width, rows, band_offset, band_stride,
+        (uint32_t)__builtin_ctz(band_rows));
+    if (hipGetLastError() != hipSuccess || hipDeviceSynchronize() != hipSuccess) return PT_ERR_HIP;
+    return PT_OK;
 }
 
 PT_API int pt_create(int device, uint32_t width, uint32_t height, uint32_t row_offset, uint32_t row_stride,

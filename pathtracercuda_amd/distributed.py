@@ -56,6 +56,18 @@ def gather_framebuffer(local, height: int, rank: int, world: int, recv=None, ful
         dist.gather(local, recv, dst=0)
         if full is None:
             full = torch.empty((height,) + tuple(local.shape[1:]), dtype=local.dtype, device=local.device)
+        if local.device.type == "cuda":
+            # on the GPU the scatter is the native unpermute kernel -- the same one pt_group_gather
+            # runs after its RCCL gather -- so both multi-GPU front ends assemble the image identically
+            from . import _native as N
+            width = int(local.shape[1])
+            for r in range(world):
+                rc = N.hip().pt_unpermute_bands(int(local.device.index or 0), full.data_ptr(), recv[r].data_ptr(), width,
+                                                int(height), int(band_rows), r, int(world))
+                if rc != 0:
+                    raise RuntimeError(f"pt_unpermute_bands failed ({rc})")
+            return full
+        # CPU tensors (the gloo tests): the same row map (global_rows), as a torch index copy
         for r in range(world):
             idx = index[r] if index is not None else torch.tensor(global_rows(height, r, world, band_rows),
                                                                   dtype=torch.long, device=local.device)

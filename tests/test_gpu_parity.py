@@ -564,3 +564,30 @@ def test_cli_headless_outputs(gpu_available, tmp_path, scenes):
     tol = np.nan_to_num(want[..., :3]).max(-1, keepdims=True) / 128.0 + 1e-30
     finite = np.isfinite(want).all(-1)
     assert (np.abs(back[..., :3] - want[..., :3])[finite] <= tol[finite]).all()
+
+
+def test_torchrun_unpermute_matches_row_map(gpu_available, root):
+    # the one-process-per-GPU gather scatters with the native unpermute kernel (pt_unpermute_bands,
+    # the kernel pt_group_gather runs); it must place every band as global_rows() says.  torch is
+    # imported first in its own process (one HIP runtime per process)
+    import subprocess
+    import sys
+    code = (
+        "import torch\n"
+        "from pathtracercuda_amd import _native as N\n"
+        "from pathtracercuda_amd.distributed import global_rows, max_rows\n"
+        "W = 72\n"
+        "for H, world, band in ((64, 3, 8), (61, 2, 8), (37, 4, 1)):\n"
+        "    g = torch.Generator().manual_seed(H)\n"
+        "    full = torch.full((H, W, 4), -1.0, device='cuda')\n"
+        "    want = torch.full((H, W, 4), -1.0)\n"
+        "    for r in range(world):\n"
+        "        part = torch.rand((max_rows(H, world, band), W, 4), generator=g)\n"
+        "        idx = torch.tensor(global_rows(H, r, world, band), dtype=torch.long)\n"
+        "        want.index_copy_(0, idx, part[: idx.numel()])\n"
+        "        pd = part.cuda()\n"
+        "        assert N.hip().pt_unpermute_bands(0, full.data_ptr(), pd.data_ptr(), W, H, band, r, world) == 0\n"
+        "    assert torch.equal(full.cpu().view(torch.int32), want.view(torch.int32)), (H, world, band)\n"
+        "print('ok')\n")
+    r = subprocess.run([sys.executable, "-c", code], capture_output=True, text=True, cwd=str(root), timeout=120)
+    assert r.returncode == 0 and r.stdout.strip().endswith("ok"), (r.stdout, r.stderr)
