@@ -44,9 +44,9 @@ for step in "$@"; do
         i=$((i+1))
         for w in ${PMC:-c3 c2 c5}; do
           case $w in
-            c3) cmd="$R/bench.py --steps 1 --warmup 0 --cpu-baseline 0 --secondary 0";;
-            c2) cmd="$R/tools/one_launch.py --scene cornell_box --width 512 --height 512 --spp 64";;
-            c5) cmd="$R/bench.py --config C5 --steps 1 --warmup 0 --cpu-baseline 0 --secondary 0";;
+            c3) cmd="$R/bench.py --steps 1 --warmup 1 --cpu-baseline 0 --secondary 0";;
+            c2) cmd="$R/tools/one_launch.py --scene cornell_box --width 512 --height 512 --spp 64 --reps 2";;
+            c5) cmd="$R/bench.py --config C5 --steps 1 --warmup 1 --cpu-baseline 0 --secondary 0";;
           esac
           mkdir -p "$O/pmc_$w"; echo "$SHA" > "$O/pmc_$w/kernel_sha.txt"
           echo "== pmc $w $i: $grp"
