@@ -76,7 +76,7 @@ struct TraceParams {
     const float4* cnodes;       // child-box records (4 per interior node), see traverse_cb
     uint32_t cnodeCount, rootWord;
     const float4* qnodes;       // 4-wide child-box records (8 per even-depth interior node), see walk_interior_quad
-    uint32_t qnodeCount, qrootWord;
+    uint32_t qnodeCount, qrootWord, qstackDepth;
     float rootBox[6];           // (min.x, max.x, min.y, max.y, min.z, max.z) of the root
     const uint32_t* order;      // tile dispatch order as packed tile coordinates (tileY << 16 | tileX),
                                 // see "Tile scheduling"; null only with scatterWaves
@@ -1476,12 +1476,12 @@ __global__ void __launch_bounds__(WPB * 64, MINW) trace_kernel(TraceParams P)
     constexpr bool SSG = MODE == 1, AUX = MODE == 2;
     const uint32_t lane = threadIdx.x & 63u;
     const uint32_t wave = threadIdx.x >> 6;
-    // QUAD (WW / 100000 == 1): the 4-wide child-box walk over qnodes (walk_interior_quad), whose
-    // unconditional stack writes reach one slot above the reference's pending count
+    // QUAD (WW / 100000 == 1): the 4-wide child-box walk over qnodes (walk_interior_quad), with its
+    // own stack bound (pt_set_scene)
     constexpr bool QUAD = WW >= 100 && (WW / 100000) % 10 == 1;
     const float4* gnodes = QUAD ? P.qnodes : (WW >= 3 ? P.cnodes : P.nodes);
     const uint32_t nodeF4 = QUAD ? 8u * P.qnodeCount : (WW >= 3 ? 4u * P.cnodeCount : 2u * P.nodeCount);
-    const uint32_t stackDepth = P.stackDepth + (QUAD ? 1u : 0u);
+    const uint32_t stackDepth = QUAD ? P.qstackDepth : P.stackDepth;
     const uint32_t sceneF4 = (SL >= 1 ? nodeF4 : 0u) + (SL >= 2 ? 4u * P.primCount : 0u);
     if (SL >= 1) {
         for (uint32_t i = threadIdx.x; i < nodeF4; i += WPB * 64) lds4[i] = gnodes[i];
@@ -2003,7 +2003,7 @@ struct pt_context {
     float4* cnodes = nullptr;   // child-box records (traverse_cb); null when the scene exceeds its encoding
     uint32_t cnodeCount = 0, rootWord = 0;
     float4* qnodes = nullptr;   // 4-wide child-box records (walk_interior_quad); null when boxes are not nested
-    uint32_t qnodeCount = 0, qrootWord = 0;
+    uint32_t qnodeCount = 0, qrootWord = 0, qstackDepth = 1;
     float rootBox[6] = {};
     uint32_t nodeCount = 0, primCount = 0, stackDepth = 1;
     bool slabFast = true;
@@ -2093,7 +2093,7 @@ static hipError_t launch_one(const TraceParams& P, hipStream_t stream)
         return launch_one<STATS, SL, WPB, WW % 100000, MINW, PERSIST, MODE>(P, stream);
     const size_t nodeF4 = QUAD ? 8 * (size_t)P.qnodeCount : (WW >= 3 ? 4 * (size_t)P.cnodeCount : 2 * (size_t)P.nodeCount);
     const size_t sceneBytes = ((SL >= 1 ? nodeF4 : 0) + (SL >= 2 ? 4 * (size_t)P.primCount : 0)) * sizeof(float4);
-    const size_t lds = sceneBytes + (size_t)WPB * (P.stackDepth + (QUAD ? 1 : 0)) * 64 * (WW >= 3 ? 8 : 4) + (size_t)WPB * 64 * 12;
+    const size_t lds = sceneBytes + (size_t)WPB * (QUAD ? P.qstackDepth : P.stackDepth) * 64 * (WW >= 3 ? 8 : 4) + (size_t)WPB * 64 * 12;
     if (WW >= 3 && P.cnodes == nullptr) return MODE == 1 ? hipErrorInvalidValue : launch_one<STATS, SL, WPB, 1, MINW, PERSIST, MODE>(P, stream);  // no child-box layout
     if (lds > 160 * 1024) {
         // scene too large to stage in LDS: the same variant reading the scene through the caches
@@ -2547,8 +2547,33 @@ PT_API int pt_set_scene(pt_context* ctx, const pt_bvh_node* nodes, uint32_t node
     ctx->nodeCount = node_count;
     ctx->primCount = prim_count;
     ctx->slabFast = slabFast;
-    // a traversal holds at most one pending sibling per interior ancestor: depth - 1 entries
-    ctx->stackDepth = maxDepth > 1 ? maxDepth - 1 : 1;
+    // LDS stack rows.  A lane visiting node v holds at most pend(v) pending entries: the ancestors
+    // whose near child (trace.cu:69-76, by the sign of the ray direction along their split axis) is
+    // on the path to v -- their far child is pushed.  The walks write one entry unconditionally
+    // above the top at an interior visit (walk_interior, and the node-at-a-time walks push there),
+    // two at a 4-wide landing visit, one at a pair visit, so the rows needed are the maximum over
+    // the 8 direction octants of pend(v) + 1 over interior v (2-wide) and pend(v) + 2 over landing /
+    // pend(v) + 1 over odd-depth nodes (4-wide).  pend(v) <= depth(v) - 1, the reference's bound.
+    {
+        std::vector<uint8_t> pend(node_count), odd(node_count, 0);
+        uint32_t need2 = 1, needQ = 1;
+        for (uint32_t o = 0; o < 8; ++o) {
+            pend[0] = 0;
+            for (uint32_t i = 0; i < node_count; ++i) {
+                const uint32_t pca = nodes[i].primitive_count_axis;
+                if ((pca >> 16) != 0) continue;
+                const bool neg = (o >> ((pca >> 8) & 0xffu)) & 1u;
+                const uint32_t a = i + 1, b = nodes[i].offset;
+                pend[neg ? b : a] = (uint8_t)(pend[i] + 1);
+                pend[neg ? a : b] = pend[i];
+                odd[a] = odd[b] = (uint8_t)(odd[i] ^ 1u);
+                need2 = std::max<uint32_t>(need2, pend[i] + 1u);
+                needQ = std::max<uint32_t>(needQ, pend[i] + (odd[i] ? 1u : 2u));
+            }
+        }
+        ctx->stackDepth = std::min(need2, maxDepth > 1 ? maxDepth - 1 : 1u);
+        ctx->qstackDepth = needQ;
+    }
     return PT_OK;
 }
 
@@ -2590,11 +2615,13 @@ PT_API int pt_set_skybox(pt_context* ctx, uint32_t handle)
 // (1.5 tiles per slot or more: the cost-sorted list schedule balances well enough).
 static uint32_t ssg_groups(const pt_context* ctx, int variant, uint32_t tiles, uint32_t total)
 {
-    if (ctx->ssgMode == 1 || (variant != 39 && variant != 40 && variant != 41 && variant != 46)) return 0;
+    if (ctx->ssgMode == 1 || (variant != 39 && variant != 40 && variant != 41 && variant != 46 && variant != 59 &&
+                              variant != 60 && variant != 61 && variant != 66))
+        return 0;
     if (ctx->ssgMode >= 2) return std::min<uint32_t>((uint32_t)ctx->ssgMode, std::max(total, 1u));
     int cus = 0;
     if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, ctx->device) != hipSuccess) return 0;
-    const uint64_t resident = (uint64_t)cus * 4 * (variant == 46 ? 4 : 5);
+    const uint64_t resident = (uint64_t)cus * 4 * (variant == 46 || variant == 66 ? 4 : 5);
     uint64_t g = (6 * resident + tiles - 1) / tiles;
     g = std::min<uint64_t>({g, 8, total / 64});
     // measured (tools/ssg_probe.py): with 2 or 3 groups the logging, the fold and the
@@ -2618,6 +2645,30 @@ static int small_grid_variant(const pt_context* ctx, int variant, uint32_t tiles
     const size_t group = 4 * (size_t)ctx->cnodeCount * sizeof(float4) + 4 * (size_t)ctx->primCount * sizeof(float4) +
                          4 * (size_t)ctx->stackDepth * 64 * 8 + 4 * 64 * 12;
     return 4 * group <= 160 * 1024 ? 48 : 47;
+}
+
+// The 4-wide walk (walk_interior_quad) in place of the 2-wide one when the scene has the 4-wide
+// layout and its records and stacks take no more LDS per workgroup than the 2-wide ones' budget
+// (occupancy unchanged): 39 -> 59, 40 -> 60, 41 -> 61, 46 -> 66, 47 -> 67.
+constexpr bool kQuadDefault = false;
+
+static int quad_variant(const pt_context* ctx, int variant, uint32_t tiles)
+{
+    (void)tiles;
+    if (!kQuadDefault || !ctx->qnodes) return variant;
+    const size_t slices = 4 * 64 * 12;
+    const size_t q = 4 * (size_t)ctx->qstackDepth * 64 * 8 + slices;
+    const size_t c = 4 * (size_t)ctx->stackDepth * 64 * 8 + slices;
+    const size_t qRec = 8 * (size_t)ctx->qnodeCount * sizeof(float4), cRec = 4 * (size_t)ctx->cnodeCount * sizeof(float4);
+    switch (variant) {
+    case 39: case 40: case 47:                     // records staged in LDS
+        if (qRec + q > cRec + c && (qRec + q) * (variant == 47 ? 4 : 5) > 160 * 1024) return variant;
+        return variant == 39 ? 59 : (variant == 40 ? 60 : 67);
+    case 41: case 46:                              // records read through the caches
+        if (q > c && q * (variant == 46 ? 4 : 5) > 160 * 1024) return variant;
+        return variant == 41 ? 61 : 66;
+    default: return variant;
+    }
 }
 
 // Grow-only device buffers of the speculative groups; false if the device is out of memory (the
@@ -2847,6 +2898,7 @@ static int render_impl(pt_context* ctx, const pt_camera* cam, uint32_t spp, uint
     P.qnodes = ctx->qnodes;
     P.qnodeCount = ctx->qnodeCount;
     P.qrootWord = ctx->qrootWord;
+    P.qstackDepth = ctx->qstackDepth;
     for (int k = 0; k < 6; ++k) P.rootBox[k] = ctx->rootBox[k];
     // Tile scheduling: a pixel's samples are sequential (one XORWOW stream), so a tile is the
     // smallest unit of work, and tiles differ several-fold in cost (sky vs geometry).  Every
@@ -2942,6 +2994,7 @@ static int render_impl(pt_context* ctx, const pt_camera* cam, uint32_t spp, uint
             (uint64_t)tiles <= (uint64_t)cus * 4 * 5)
             variant = 39;
     }
+    if (ctx->variant == 0) variant = quad_variant(ctx, variant, tiles);
     ctx->lastGroups = 0;
     memset(ctx->groupStats, 0, sizeof(ctx->groupStats));
     ++ctx->epoch;
