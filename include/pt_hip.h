@@ -234,6 +234,11 @@ PT_API int pt_set_issue_priority(pt_context *ctx, int mode, uint32_t level3, uin
  * ([tile][2G - 1][64], tiles in dispatch (cost) order; item 0 = group 0, items 2g - 1 and 2g =
  * group g at its guessed offset and one draw pair later).  pt_set_patch_rounds: patch rounds before
  * the remaining dead ends run as a plain resume launch (default 6; 0 exercises the resume path). */
+/* Tuning knob: tiles per dispatch unit of launches with few samples per pixel (a row strip of K
+ * tiles; a lane whose pixel is done takes the same position in the next tile of its strip).
+ * 0 = automatic (K = 2 at <= 64 samples per pixel on large images), 1 = off, K = 2..16 = always K
+ * (resumable variants).  Results are identical for every setting. */
+PT_API int pt_set_strip_units(pt_context *ctx, int mode);
 PT_API int pt_set_sample_groups(pt_context *ctx, int mode);
 PT_API int pt_set_patch_rounds(pt_context *ctx, uint32_t rounds);
 PT_API int pt_last_sample_groups(const pt_context *ctx);

@@ -317,6 +317,11 @@ class Pathtracer:
         for c in self._contexts():
             N.check_ctx(N.hip().pt_set_schedule(c, int(mode)), c)
 
+    def set_strip_units(self, mode: int) -> None:
+        """pt_set_strip_units on every device context (0 automatic, 1 off, K >= 2 always K tiles per unit)."""
+        for c in self._contexts():
+            N.check_ctx(N.hip().pt_set_strip_units(c, int(mode)), c)
+
     def set_sample_groups(self, mode: int) -> None:
         """Speculative sample groups (pt_set_sample_groups): 0 = automatic, 1 = off, G >= 2 = always G."""
         for c in self._contexts():

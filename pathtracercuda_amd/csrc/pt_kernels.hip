@@ -109,6 +109,7 @@ struct TraceParams {
     DevCamera cam;
     uint32_t occCap;            // host only: persistent grids hold at most this many workgroups per CU (0 = all)
     uint32_t prio[3];           // issue priority by order position: < prio[0] -> 3, < prio[1] -> 2, < prio[2] -> 1
+    uint32_t strip;             // MODE 3: tiles per dispatch unit (a row strip of `strip` tiles; see trace_kernel)
 };
 
 // Speculative sample groups: window of a group's start offset in which an earlier group's parse can
@@ -1473,7 +1474,7 @@ PT_DEV void store_pixel(const TraceParams& P, const PixelCtx& pc, const Xorwow& 
 template <bool STATS, int SL, int WPB, int WW, int MINW, bool PERSIST = false, int MODE = 0>
 __global__ void __launch_bounds__(WPB * 64, MINW) trace_kernel(TraceParams P)
 {
-    constexpr bool SSG = MODE == 1, AUX = MODE == 2;
+    constexpr bool SSG = MODE == 1, AUX = MODE == 2, STRIP = MODE == 3;
     const uint32_t lane = threadIdx.x & 63u;
     const uint32_t wave = threadIdx.x >> 6;
     // QUAD (WW / 100000 == 1): the 4-wide child-box walk over qnodes (walk_interior_quad), with its
@@ -1517,7 +1518,7 @@ __global__ void __launch_bounds__(WPB * 64, MINW) trace_kernel(TraceParams P)
     else if (pos < P.prio[1]) __builtin_amdgcn_s_setprio(2);
     else if (pos < P.prio[2]) __builtin_amdgcn_s_setprio(1);
     else __builtin_amdgcn_s_setprio(0);
-    const PixelCtx pc = pixel_of(P, tile, lane);
+    PixelCtx pc = pixel_of(P, tile, lane);
     const uint64_t tWave = __builtin_amdgcn_s_memtime();
     const bool run = pc.valid && (!AUX || !P.fold || (P.fold[F_FLAG * pc.npix + pc.li] & 1u));
     if (run) {
@@ -1526,8 +1527,9 @@ __global__ void __launch_bounds__(WPB * 64, MINW) trace_kernel(TraceParams P)
         SsgLane sl;
         if (SSG) ssg_load(P, pos, grp, lane, pc.li, pc.npix, rng, ps, sl);
         else load_pixel<AUX>(P, pc, rng, ps, accL);
-        const float fx = (float)(int32_t)pc.px, fy = (float)(int32_t)pc.py;
+        float fx = (float)(int32_t)pc.px, fy = (float)(int32_t)pc.py;
         camera_ray(P, fx, fy, rng, ps.o, ps.d);
+        uint32_t stripK = 0;                     // STRIP: this lane's tile within the unit
         uint64_t tAll = STATS ? __builtin_amdgcn_s_memtime() : 0;
         uint64_t tDone = 0;
         if (WW >= 100) {
@@ -1566,6 +1568,23 @@ __global__ void __launch_bounds__(WPB * 64, MINW) trace_kernel(TraceParams P)
                 if (shade<STATS>(P, prims, ts.elem, ts.tMax, ps, rng, cnt)) {
                     if (SSG) ssg_finish<STATS>(P, ps, rng, fx, fy, sl, lane, cnt);
                     else finish_path<STATS>(P, ps, rng, fx, fy, cnt);
+                    if (STRIP && !ps.alive && stripK + 1 < P.strip) {
+                        // Strip units (launches of few samples per pixel): a lane whose pixel is done
+                        // stores it and takes the same position in the unit's next tile -- the tile to
+                        // the right, so the wave's rays stay spatially coherent -- instead of idling
+                        // until the slowest pixel of its tile is done.  Pixels are independent
+                        // (their own RNG stream and accumulation value): results are unchanged.
+                        const PixelCtx nx = pixel_of(P, tile + stripK + 1, lane);
+                        if (nx.valid) {
+                            store_pixel(P, pc, rng, ps);
+                            pc = nx;
+                            ++stripK;
+                            load_pixel<false>(P, pc, rng, ps, accL);
+                            fx = (float)(int32_t)pc.px;
+                            fy = (float)(int32_t)pc.py;
+                            camera_ray(P, fx, fy, rng, ps.o, ps.d);
+                        }
+                    }
                 }
                 if (STATS) wave_time(cnt.cyc_shade, tS);
                 if (STATS && !ps.alive) tDone = __builtin_amdgcn_s_memtime();
@@ -1603,6 +1622,10 @@ __global__ void __launch_bounds__(WPB * 64, MINW) trace_kernel(TraceParams P)
         const uint32_t lin = (tile >> 16) * P.tilesX + (tile & 0xffffu);
         if (SSG) atomicAdd(&P.tileCost[lin], cyc / P.ssgG);   // zeroed before the launch (idle items add ~0)
         else P.tileCost[lin] = cyc;
+        // STRIP: the unit's cost sits at its first tile, the other tiles' entries are 0, so a sort of
+        // the tile costs lists the units first (pt_render: the order of a strip launch)
+        if (STRIP)
+            for (uint32_t k = 1; k < P.strip && (tile & 0xffffu) + k < P.tilesX; ++k) P.tileCost[lin + k] = 0u;
     }
     if (!PERSIST) break;
     slot = wave_fetch(P.tileCursor, 1u);
@@ -2028,6 +2051,10 @@ struct pt_context {
     bool orderStale = true;       // rebuild it after the next launch (scene, texture or camera changed)
     uint64_t orderSamples = 0;    // samples per pixel of the launch whose tile costs built `order`
     int schedule = 0;             // 0 = cost-sorted tiles (default), 1 = row-major
+    int stripMode = 0;            // strip units: 0 = automatic, 1 = off, K >= 2 = always K tiles per unit
+    uint32_t orderStrip = 1;      // tiles per unit of the launch whose costs built `order`
+    uint32_t* unitMajor = nullptr;    // row-major order of strip units (packed first tiles), for unitK
+    uint32_t unitK = 0, unitTiles = 0;
     uint32_t occupancy = 0;       // tuning knob: workgroups per CU of persistent grids (0 = all that fit)
     int prioMode = 0;             // issue priority: 0 = automatic, 1 = off, 2 = explicit bounds prioBounds
     uint32_t prioBounds[3] = {0, 0, 0};
@@ -2206,6 +2233,42 @@ static hipError_t launch_grouped(int v, const TraceParams& P, hipStream_t stream
     }
 }
 
+// Strip-unit launches (MODE 3) of the resumable persistent variants.
+static hipError_t launch_strip(int v, const TraceParams& P, hipStream_t stream)
+{
+    switch (v) {
+    case 40: return launch_one<false, 1, 4, kV40Walk, 5, true, 3>(P, stream);
+    case 41: return launch_one<false, 0, 4, 14212, 5, true, 3>(P, stream);
+    case 46: return launch_one<false, 0, 4, 14212, 4, true, 3>(P, stream);
+    case 60: return launch_one<false, 1, 4, 100000 + kV40Walk, 5, true, 3>(P, stream);
+    case 61: return launch_one<false, 0, 4, 100000 + 14212, 5, true, 3>(P, stream);
+    case 66: return launch_one<false, 0, 4, 100000 + 14212, 4, true, 3>(P, stream);
+    default: return hipErrorInvalidValue;
+    }
+}
+
+static bool strip_capable(int v) { return v == 40 || v == 41 || v == 46 || v == 60 || v == 61 || v == 66; }
+
+// Tiles per dispatch unit.  A launch of few samples per pixel (the reference's 8-spp render() calls,
+// 1-spp progressive frames) idles the lanes whose pixels finish first for the rest of their tile
+// (23 % of lane time at 8 spp against 6 % at 1024); strips of K tiles let those lanes
+// go on with the next tile.  Automatic: K = 2 for launches of at most 64 samples per pixel that
+// keep at least ~3 units per wave slot; the variant must be a strip-capable one.
+constexpr uint64_t kStripMaxSamples = 64;
+
+static uint32_t strip_tiles(const pt_context* ctx, int variant, uint32_t tiles, uint64_t samples)
+{
+    if (ctx->stripMode == 1) return 1;
+    const int v = ctx->variant ? ctx->variant : variant;
+    if (!strip_capable(v) && !(ctx->variant == 0 && (v == 40 || v == 41 || v == 46))) return 1;
+    if (ctx->stripMode >= 2) return (uint32_t)ctx->stripMode;
+    if (samples > kStripMaxSamples) return 1;
+    int cus = 0;
+    if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, ctx->device) != hipSuccess) return 1;
+    const uint64_t slots = (uint64_t)cus * 4 * 5;
+    return (uint64_t)tiles >= 6 * slots ? 2u : 1u;
+}
+
 static bool variant_shipped(int v)
 {
     return v == 0 || v == 1 || v == 4 || v == 6 || v == 20 || v == 40 || v == 41 || v == 46 || v == 47 || v == 48 || v == 39 ||
@@ -2350,6 +2413,7 @@ PT_API void pt_destroy(pt_context* ctx)
     (void)hipFree(ctx->tileIdle);
     (void)hipFree(ctx->order);
     (void)hipFree(ctx->rowMajor);
+    (void)hipFree(ctx->unitMajor);
     (void)hipFree(ctx->tileCursor);
     (void)hipFree(ctx->ldr);
     (void)hipFree(ctx->sortKeys);
@@ -2755,9 +2819,10 @@ static void ssg_release(pt_context* ctx)
 
 // Stable radix sort of (cost, tile) pairs, descending, into the dispatch order: deterministic, ties
 // in tile order.
-static int sort_order(pt_context* ctx, uint32_t tiles, uint64_t samples)
+static int sort_order(pt_context* ctx, uint32_t tiles, uint64_t samples, uint32_t strip)
 {
     ctx->orderSamples = samples;
+    ctx->orderStrip = strip;
     size_t bytes = ctx->sortTempBytes;
     PT_HIP_CHECK(ctx, rocprim::radix_sort_pairs_desc(ctx->sortTemp, bytes, ctx->tileCost, ctx->sortKeys, ctx->tileIds,
                                                      ctx->order, tiles, 0, 32, ctx->stream));
@@ -2952,7 +3017,29 @@ static int render_impl(pt_context* ctx, const pt_camera* cam, uint32_t spp, uint
         ctx->lastCam = *cam;
     }
     const bool sorted = ctx->schedule == 0;
-    P.order = (sorted && ctx->orderValid) ? ctx->order : ctx->rowMajor;
+    // Strip units (MODE 3, trace_kernel): launches of few samples per pixel dispatch row strips of K
+    // tiles, and a lane whose pixel is done moves on to the next tile of its strip.  The cost order
+    // is over units, so it is rebuilt when K changes.
+    const uint32_t K = (sorted && !stats) ? strip_tiles(ctx, pick_variant(ctx), tiles, (uint64_t)spp * chunks) : 1u;
+    const uint32_t unitsX = (P.tilesX + K - 1) / K, units = unitsX * P.tilesY;
+    if (K != ctx->orderStrip) {
+        ctx->orderValid = false;
+        ctx->orderStale = true;
+    }
+    if (K > 1 && (ctx->unitK != K || ctx->unitTiles != tiles)) {
+        (void)hipFree(ctx->unitMajor);
+        ctx->unitMajor = nullptr;
+        std::vector<uint32_t> um((size_t)units + 64);
+        for (size_t i = 0; i < um.size(); ++i)
+            um[i] = i < units ? ((uint32_t)(i / unitsX) << 16) | (uint32_t)(i % unitsX * K) : P.tilesY << 16;
+        PT_HIP_CHECK(ctx, hipMalloc(&ctx->unitMajor, um.size() * sizeof(uint32_t)));
+        PT_HIP_CHECK(ctx, hipMemcpy(ctx->unitMajor, um.data(), um.size() * sizeof(uint32_t), hipMemcpyHostToDevice));
+        ctx->unitK = K;
+        ctx->unitTiles = tiles;
+    }
+    uint32_t* const firstOrder = K > 1 ? ctx->unitMajor : ctx->rowMajor;
+    P.strip = K;
+    P.order = (sorted && ctx->orderValid) ? ctx->order : firstOrder;
     P.tileCost = sorted ? ctx->tileCost : nullptr;
     P.scatterWaves = ctx->schedule == 2 ? (uint32_t)(((size_t)ctx->rows * ctx->width + 63) / 64) : 0u;
     if (P.scatterWaves) P.order = nullptr;          // scattered mapping: slot = wave index
@@ -2961,7 +3048,7 @@ static int render_impl(pt_context* ctx, const pt_camera* cam, uint32_t spp, uint
         PT_HIP_CHECK(ctx, hipMemset(ctx->tileCursor, 0, 2 * sizeof(uint32_t)));
     }
     P.tileCursor = ctx->tileCursor;
-    P.numSlots = tiles;
+    P.numSlots = units;
     P.occCap = ctx->occupancy;
     // Issue priority follows the order position, so it is meaningful only on a current cost order.
     // A launch whose tile costs will rebuild the order (stale order, or this launch measures >= 4x
@@ -2970,7 +3057,7 @@ static int render_impl(pt_context* ctx, const pt_camera* cam, uint32_t spp, uint
     // on every rebuild (a feedback the order would carry over camera moves).
     const bool rebuilds = ctx->schedule == 0 &&
                           (ctx->orderStale || !ctx->orderValid || (uint64_t)spp * chunks >= 4 * ctx->orderSamples);
-    if (!rebuilds || ctx->prioMode == 2) issue_priority(ctx, tiles, P.prio);   // explicit bounds: always
+    if (!rebuilds || ctx->prioMode == 2) issue_priority(ctx, units, P.prio);   // explicit bounds: always
     if (stats) {
         PT_HIP_CHECK(ctx, hipMemsetAsync(ctx->stats, 0, kStatWords * sizeof(unsigned long long), ctx->stream));
         if (!ctx->tileIdle) PT_HIP_CHECK(ctx, hipMalloc(&ctx->tileIdle, (size_t)tiles * sizeof(uint32_t)));
@@ -2982,7 +3069,7 @@ static int render_impl(pt_context* ctx, const pt_camera* cam, uint32_t spp, uint
     const uint32_t total = spp * chunks;
     // the fold state packs (sample in call, call) into one word as sIdx | c << 16 (ssg_fold_kernel)
     const bool groupable = !stats && sorted && (uint64_t)spp * chunks < (1ull << 31) && spp <= 0xffffu && chunks <= 0xffffu;
-    uint32_t G = groupable ? ssg_groups(ctx, variant, tiles, total) : 0;
+    uint32_t G = groupable && K == 1 ? ssg_groups(ctx, variant, tiles, total) : 0;
     if (!G && ctx->variant == 0) variant = small_grid_variant(ctx, variant, tiles);
     // Grouped launches of at most one tile per wave slot (one rank's 1080p share at N = 8) are
     // short items whose latency sets the launch: deferred shading, which trades a lane's latency for
@@ -3024,12 +3111,13 @@ static int render_impl(pt_context* ctx, const pt_camera* cam, uint32_t spp, uint
         Q.chunks = 1;
         Q.ignoreFirst = 1;
         Q.discard = 1;
-        Q.order = ctx->rowMajor;
+        Q.order = firstOrder;
         for (int i = 0; i < 3; ++i) Q.prio[i] = 0;        // row-major positions: no priority grading
         Q.pairsOut = guesses && ssg_reserve(ctx, tiles, 0, 0, 0) ? ctx->pairs : nullptr;
         if (Q.pairsOut) ctx->pairsValid = true;
-        PT_HIP_CHECK(ctx, Q.pairsOut ? launch_grouped<2>(variant, Q, ctx->stream) : launch_variant<false>(variant, Q, ctx->stream));
-        const int rs = sort_order(ctx, tiles, Q.spp);
+        PT_HIP_CHECK(ctx, Q.pairsOut ? launch_grouped<2>(variant, Q, ctx->stream)
+                                     : (K > 1 ? launch_strip(variant, Q, ctx->stream) : launch_variant<false>(variant, Q, ctx->stream)));
+        const int rs = sort_order(ctx, tiles, Q.spp, K);
         if (rs != PT_OK) return rs;
         P.order = ctx->order;
     }
@@ -3039,7 +3127,8 @@ static int render_impl(pt_context* ctx, const pt_camera* cam, uint32_t spp, uint
         if (rc != PT_OK) return rc;
         ctx->lastGroups = G;
     } else {
-        PT_HIP_CHECK(ctx, stats ? launch_variant<true>(variant, P, ctx->stream) : launch_variant<false>(variant, P, ctx->stream));
+        PT_HIP_CHECK(ctx, stats ? launch_variant<true>(variant, P, ctx->stream)
+                                : (K > 1 ? launch_strip(variant, P, ctx->stream) : launch_variant<false>(variant, P, ctx->stream)));
     }
     PT_HIP_CHECK(ctx, hipGetLastError());
     PT_HIP_CHECK(ctx, hipEventRecord(ctx->ev1, ctx->stream));
@@ -3052,7 +3141,7 @@ static int render_impl(pt_context* ctx, const pt_camera* cam, uint32_t spp, uint
     // start's 2-spp pre-pass, an 8-spp first launch): short launches rank tiles noisily, and a heavy
     // tile ranked light is dispatched late and becomes the launch's tail.
     if (sorted && (ctx->orderStale || !ctx->orderValid || total >= 4 * ctx->orderSamples)) {
-        const int rs = sort_order(ctx, tiles, total);
+        const int rs = sort_order(ctx, tiles, total, K);
         if (rs != PT_OK) return rs;
     }
     if (stats) {
@@ -3081,6 +3170,13 @@ static int render_impl(pt_context* ctx, const pt_camera* cam, uint32_t spp, uint
         stats->leaf_pairs = h[20];
         stats->family_execs_compacted_in_round = h[21];
     }
+    return PT_OK;
+}
+
+PT_API int pt_set_strip_units(pt_context* ctx, int mode)
+{
+    if (!ctx || mode < 0 || mode > 16) return PT_ERR_ARG;
+    ctx->stripMode = mode;
     return PT_OK;
 }
 

@@ -591,3 +591,26 @@ def test_torchrun_unpermute_matches_row_map(gpu_available, root):
         "print('ok')\n")
     r = subprocess.run([sys.executable, "-c", code], capture_output=True, text=True, cwd=str(root), timeout=120)
     assert r.returncode == 0 and r.stdout.strip().endswith("ok"), (r.stdout, r.stderr)
+
+
+@pytest.mark.parametrize("W,H,band", [(1280, 720, 0), (1004, 604, 0), (1920, 1080, 3)])
+def test_strip_units_bitexact(gpu_available, scenes, W, H, band):
+    # strip units (a lane whose pixel is done moves on to the next tile of its row strip) change
+    # which lane renders a pixel, never how: every K gives the unit-less launch's bits, for 8-spp
+    # calls with and without history and for 1-spp frames, on odd image sizes (partial tiles, strips
+    # cut by the right edge) and on a band tile (row offset 3 of 8, as a rank's share)
+    pt = (pa.Pathtracer(W, H, row_offset=band, row_stride=8, band_rows=8) if band
+          else pa.Pathtracer(W, H))
+    cam = pt.load_scene(scenes / "generated_scene.scene.json")
+    st = pt.rng_state()
+    want = None
+    for K in (1, 2, 3, 4):
+        pt.set_strip_units(K)
+        pt.set_rng_state(st)
+        pt.render(cam, 8, True)
+        pt.render(cam, 8, False)
+        pt.render(cam, 1, False, chunks=2)
+        got = (pt.accum().view(np.uint32).copy(), pt.rng_state())
+        if want is None:
+            want = got
+        assert np.array_equal(got[0], want[0]) and np.array_equal(got[1], want[1]), f"strip K={K}"

@@ -1,0 +1,72 @@
+"""The reference's headless loop unchanged (main.cpp:272-279: spp/8 separate render(cam, 8, i == 0)
+calls, one synchronous launch each) against the same work as one chunked launch, for trace-kernel
+variants and strip-unit settings (pt_set_strip_units), in one process, interleaved rounds; results
+cross-checked bit-identical.
+    python tools/call_loop.py [--variants 0] [--strips 1,2,4] [--spp 1024] [--rounds 3] [--fps 1]
+"""
+import argparse
+import json
+import pathlib
+import sys
+import time
+
+import numpy as np
+
+ROOT = pathlib.Path(__file__).resolve().parents[1]
+sys.path.insert(0, str(ROOT))
+import pathtracercuda_amd as pa  # noqa: E402
+
+ap = argparse.ArgumentParser()
+ap.add_argument("--scene", default=str(ROOT / "scenes/generated_scene.scene.json"))
+ap.add_argument("--width", type=int, default=1920)
+ap.add_argument("--height", type=int, default=1080)
+ap.add_argument("--spp", type=int, default=1024)
+ap.add_argument("--rounds", type=int, default=3)
+ap.add_argument("--variants", default="0")
+ap.add_argument("--strips", default="1,2,4")
+ap.add_argument("--frames", type=int, default=0, help="also time this many 1-spp progressive frames per setting")
+a = ap.parse_args()
+pt = pa.Pathtracer(a.width, a.height)
+cam = pt.load_scene(a.scene)
+st = pt.rng_state()
+settings = [(int(v), int(k)) for v in a.variants.split(",") for k in a.strips.split(",")]
+res = {f"{v}/k{k}": {"loop_ms": [], "gpu_ms": [], "frame_ms": []} for v, k in settings}
+ref = None
+for r in range(a.rounds):
+    for v, k in settings:
+        pt.set_kernel_variant(v)
+        pt.set_strip_units(k)
+        pt.set_rng_state(st)
+        t0 = time.perf_counter()
+        g = 0.0
+        for i in range(a.spp // 8):
+            pt.render(cam, 8, i == 0)
+            g += pt.get_timing()
+        res[f"{v}/k{k}"]["loop_ms"].append((time.perf_counter() - t0) * 1e3)
+        res[f"{v}/k{k}"]["gpu_ms"].append(g)
+        acc = pt.accum().view(np.uint32)
+        if ref is None:
+            ref = acc.copy()
+        assert np.array_equal(acc, ref), f"variant {v} strip {k} differs"
+        if a.frames:
+            t0 = time.perf_counter()
+            for f in range(a.frames):
+                pt.render(cam, 1, f == 0)
+            res[f"{v}/k{k}"]["frame_ms"].append((time.perf_counter() - t0) * 1e3 / a.frames)
+pt.set_strip_units(0)
+pt.set_kernel_variant(0)
+pt.set_rng_state(st)
+fused = []
+for r in range(a.rounds):
+    pt.set_rng_state(st)
+    fused.append(pt.render_raw(cam, 8, a.spp // 8, True))
+out = {"image": f"{a.width}x{a.height}", "spp": a.spp, "calls": a.spp // 8, "fused_ms_median": float(np.median(fused)),
+       "settings": {}}
+for key, d in res.items():
+    m = float(np.median(d["loop_ms"]))
+    out["settings"][key] = {"loop_ms_median": round(m, 2), "gpu_ms_median": round(float(np.median(d["gpu_ms"])), 2),
+                            "loop_over_fused": round(m / out["fused_ms_median"], 4),
+                            "Msamples_s": round(a.width * a.height * a.spp / m / 1e3, 1)}
+    if d["frame_ms"]:
+        out["settings"][key]["frame_ms_median"] = round(float(np.median(d["frame_ms"])), 4)
+print(json.dumps(out))
