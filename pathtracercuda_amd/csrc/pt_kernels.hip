@@ -664,10 +664,11 @@ PT_DEV bool walk_interior(const float4* __restrict__ cnodes, uint2* stack, const
 // child-box format above:
 //   half 0 = N's first child A = N + 1:  A interior -> A's two children (A + 1, A.offset) with their
 //            boxes and words and 1 << A's split axis; A a leaf -> slot L = A itself, slot R empty
-//   half 1 = N's second child B = N.offset, the same;   half 0's Q3.w = 1 << N's split axis.
+//   half 1 = N's second child B = N.offset, the same.
 // A child word is (count << 24 | prim offset) for a leaf, the record index of an even-depth
-// interior node, or a PAIR reference (1 << 23 | 2 r + h): "half h of record r" -- the odd-depth
-// node whose two children that half holds.  An empty slot has the box [+inf, +inf]^3, which no ray
+// interior node with that node's split axis at bit 20 (axis << 20 | r, r < 2^20), or a PAIR
+// reference (1 << 23 | 2 r + h): "half h of record r" -- the odd-depth node whose two children that
+// half holds.  An empty slot has the box [+inf, +inf]^3, which no ray
 // hits in either slab form.
 //
 // A landing visit tests the four grandchild boxes (or the leaf children) at once, with one 128-byte
@@ -688,6 +689,9 @@ PT_DEV bool walk_interior(const float4* __restrict__ cnodes, uint2* stack, const
 // reference's; the stack holds at most the reference's pending count (<= one entry per level).
 // ---------------------------------------------------------------------------------------------
 constexpr uint32_t kPairBit = 1u << 23;
+constexpr uint32_t kQuadAxisShift = 20;                  // landing word: record | N's split axis << 20
+constexpr uint32_t kQuadRecMask = (1u << kQuadAxisShift) - 1u;
+constexpr uint32_t kQuadPairMask = (1u << (kQuadAxisShift + 1)) - 1u;   // pair word: 2 r + h
 
 template <bool STATS, bool ALLFAST>
 PT_DEV bool walk_interior_quad(const float4* __restrict__ qnodes, uint2* stack, const SlabRay& R, uint32_t negMask,
@@ -696,22 +700,20 @@ PT_DEV bool walk_interior_quad(const float4* __restrict__ qnodes, uint2* stack, 
     while ((cur >> 24) == 0u) {
         if (STATS) { cnt.node_tests += 2; wave_tick(cnt.w_node); }   // one visit (bench.lane_utilisation)
         const bool isPair = (cur & kPairBit) != 0u;
-        const uint32_t r = isPair ? (cur & (kPairBit - 1u)) >> 1 : cur;
-        const float4* q = qnodes + 8 * r;
-        const float4 A0 = q[0], A1 = q[1], A2 = q[2], A3 = q[3];
-        const float4 B0 = q[4], B1 = q[5], B2 = q[6], B3 = q[7];
-        const ChildPair hA = cb_pair<ALLFAST>(A0, A1, A2, A3, R, negMask, tMin, tMax);
-        const ChildPair hB = cb_pair<ALLFAST>(B0, B1, B2, B3, R, negMask, tMin, tMax);
-        // near side: by N's split axis on a landing visit (trace.cu:69-76), the referenced half on a pair visit
-        const bool nearIsB = isPair ? (cur & 1u) != 0u : (negMask & __float_as_uint(A3.w)) != 0u;
-        const ChildPair& nr = nearIsB ? hB : hA;
-        const ChildPair& fr = nearIsB ? hA : hB;
+        const uint32_t r = isPair ? (cur & (kQuadPairMask)) >> 1 : cur & kQuadRecMask;
+        // near side: by N's split axis (carried in the landing word, trace.cu:69-76), the referenced
+        // half on a pair visit -- known before the record arrives, so the halves load in visit order
+        const uint32_t nearIsB = isPair ? (cur & 1u) : (negMask >> ((cur >> kQuadAxisShift) & 3u)) & 1u;
+        const float4* qn = qnodes + 8 * r + 4 * nearIsB;
+        const float4* qf = qnodes + 8 * r + 4 * (nearIsB ^ 1u);
+        const ChildPair nr = cb_pair<ALLFAST>(qn[0], qn[1], qn[2], qn[3], R, negMask, tMin, tMax);
+        const ChildPair fr = cb_pair<ALLFAST>(qf[0], qf[1], qf[2], qf[3], R, negMask, tMin, tMax);
         const bool farOn = !isPair && fr.any;
         // descend into the near side if any of its children passes, else into the far side (same t_max)
         const bool intoNear = nr.any;
         const ChildPair& sd = intoNear ? nr : fr;
         // entry 1: the far side, below the near side's far child (pushed only when descending near)
-        const uint32_t w1 = fr.both ? (kPairBit | (2u * r + (nearIsB ? 0u : 1u))) : fr.wNext;
+        const uint32_t w1 = fr.both ? (kPairBit | (2u * r + (nearIsB ^ 1u))) : fr.wNext;
         const float lo1 = fr.both ? __builtin_fminf(fr.loNext, fr.loF) : fr.loNext;
         stack[64u * sp] = make_uint2(w1, __float_as_uint(lo1));
         sp += (intoNear && farOn) ? 1u : 0u;
@@ -2534,11 +2536,12 @@ PT_API int pt_set_scene(pt_context* ctx, const pt_bvh_node* nodes, uint32_t node
             }
             if (!depthOdd[i]) qrec[i] = quads++;
         }
-        qOk = qOk && quads < (1u << 22);
+        qOk = qOk && quads <= kQuadRecMask;
     }
     auto qword = [&](uint32_t i) {
         const uint32_t count = nodes[i].primitive_count_axis >> 16;
-        return count ? (count << 24) | nodes[i].offset : qrec[i];
+        return count ? (count << 24) | nodes[i].offset
+                     : qrec[i] | (((nodes[i].primitive_count_axis >> 8) & 0xffu) << kQuadAxisShift);
     };
     const float kInf = __builtin_inff();
     std::vector<float4> hq(qOk ? 8 * (size_t)std::max(quads, 1u) : 0, make_float4(kInf, kInf, kInf, kInf));
@@ -2561,8 +2564,7 @@ PT_API int pt_set_scene(pt_context* ctx, const pt_bvh_node* nodes, uint32_t node
                 wR = qword(nodes[c].offset);
                 axisBit = 1u << ((nodes[c].primitive_count_axis >> 8) & 0xffu);
             }
-            const uint32_t axisN = h == 0 ? 1u << ((nodes[i].primitive_count_axis >> 8) & 0xffu) : 0u;
-            q[3] = make_float4(u2f(leaf ? qword(c) : qword(c + 1)), u2f(wR), u2f(axisBit), u2f(axisN));
+            q[3] = make_float4(u2f(leaf ? qword(c) : qword(c + 1)), u2f(wR), u2f(axisBit), 0.0f);
         }
     }
     for (uint32_t i = 0; i < prim_count; ++i) {

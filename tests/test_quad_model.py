@@ -17,7 +17,7 @@ import pathtracercuda_amd as pa
 F = np.float32
 INF = F(np.inf)
 T_MIN = F(0.001)
-PAIR = 1 << 23
+PAIR = 1 << 23                  # pair word: PAIR | 2 r + h; landing word: r | split axis << 20
 
 
 def box(n):
@@ -93,7 +93,8 @@ def reference_walk(nodes, o, d, ray_id):
 
 def build_quads(nodes):
     """pt_set_scene's qnodes: per even-depth interior node two halves of (L box, R box, wL, wR, axis
-    bit), half 0 also N's axis bit; empty slot R of a leaf side = [+inf, +inf]^3."""
+    bit); a landing word carries its node's split axis at bit 20; empty slot R of a leaf side =
+    [+inf, +inf]^3."""
     n = len(nodes)
     odd = [0] * n
     qrec = [None] * n
@@ -112,7 +113,7 @@ def build_quads(nodes):
 
     def word(i):
         cnt = nodes[i].primitive_count_axis >> 16
-        return (cnt << 24) | nodes[i].offset if cnt else qrec[i]
+        return (cnt << 24) | nodes[i].offset if cnt else qrec[i] | (((nodes[i].primitive_count_axis >> 8) & 0xff) << 20)
 
     recs = [None] * q
     empty = (np.full(3, INF, F), np.full(3, INF, F))
@@ -126,7 +127,7 @@ def build_quads(nodes):
             else:
                 halves.append((box(nodes[c + 1]), box(nodes[nodes[c].offset]), word(c + 1), word(nodes[c].offset),
                                1 << ((nodes[c].primitive_count_axis >> 8) & 0xff)))
-        recs[qrec[i]] = (halves, 1 << ((nodes[i].primitive_count_axis >> 8) & 0xff))
+        recs[qrec[i]] = halves
     return recs, word(0)
 
 
@@ -160,10 +161,10 @@ def quad_walk(recs, root_word, root_box, nodes, o, d, ray_id):
     while cur is not None:
         if cur >> 24 == 0:
             pair = (cur & PAIR) != 0
-            r = (cur & (PAIR - 1)) >> 1 if pair else cur
-            halves, axis_n = recs[r]
+            r = (cur & ((1 << 21) - 1)) >> 1 if pair else cur & ((1 << 20) - 1)
+            halves = recs[r]
             ha, hb = cb_pair(halves[0], o, d, negmask, tmax), cb_pair(halves[1], o, d, negmask, tmax)
-            near_b = (cur & 1) != 0 if pair else (negmask & axis_n) != 0
+            near_b = (cur & 1) != 0 if pair else ((negmask >> ((cur >> 20) & 3)) & 1) != 0
             nr, fr = (hb, ha) if near_b else (ha, hb)
             far_on = not pair and fr["any"]
             if nr["any"]:
@@ -216,7 +217,7 @@ def test_quad_walk_matches_reference_order(scene, nrays):
     nodes, _ = sc.bvh()
     nodes = list(nodes)
     recs, root_word = build_quads(nodes)
-    n_leaf_sides = sum(1 for r in recs for h in r[0] if h[3] == 0xffffffff)
+    n_leaf_sides = sum(1 for r in recs for h in r if h[3] == 0xffffffff)
     assert len(recs) >= 1
     nonempty = 0
     for k, (o, d) in enumerate(rays(nodes, nrays, 7)):
