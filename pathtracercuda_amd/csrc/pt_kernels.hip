@@ -1578,7 +1578,7 @@ __global__ void __launch_bounds__(WPB * 64, MINW) trace_kernel(TraceParams P)
                         // (their own RNG stream and accumulation value): results are unchanged.
                         const PixelCtx nx = pixel_of(P, tile + stripK + 1, lane);
                         if (nx.valid) {
-                            store_pixel(P, pc, rng, ps);
+                            if (!P.discard) store_pixel(P, pc, rng, ps);   // a cost pre-pass writes nothing
                             pc = nx;
                             ++stripK;
                             load_pixel<false>(P, pc, rng, ps, accL);

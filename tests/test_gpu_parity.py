@@ -610,6 +610,7 @@ def test_strip_units_bitexact(gpu_available, scenes, W, H, band):
         pt.render(cam, 8, True)
         pt.render(cam, 8, False)
         pt.render(cam, 1, False, chunks=2)
+        pt.render(cam, 4, False, chunks=5)     # >= 16 samples: the cold-start cost pre-pass runs first
         got = (pt.accum().view(np.uint32).copy(), pt.rng_state())
         if want is None:
             want = got
