@@ -3072,7 +3072,7 @@ static int render_impl(pt_context* ctx, const pt_camera* cam, uint32_t spp, uint
     // the fold state packs (sample in call, call) into one word as sIdx | c << 16 (ssg_fold_kernel)
     const bool groupable = !stats && sorted && (uint64_t)spp * chunks < (1ull << 31) && spp <= 0xffffu && chunks <= 0xffffu;
     uint32_t G = groupable && K == 1 ? ssg_groups(ctx, variant, tiles, total) : 0;
-    if (!G && ctx->variant == 0) variant = small_grid_variant(ctx, variant, tiles);
+    if (!G && ctx->variant == 0 && K == 1) variant = small_grid_variant(ctx, variant, tiles);
     // Grouped launches of at most one tile per wave slot (one rank's 1080p share at N = 8) are
     // short items whose latency sets the launch: deferred shading, which trades a lane's latency for
     // fuller hit-shading rounds, measured bimodal there (median 57.7-62.6 ms against 57.8-58.2 ms
