@@ -32,6 +32,7 @@ st = pt.rng_state()
 settings = [(int(v), int(k)) for v in a.variants.split(",") for k in a.strips.split(",")]
 res = {f"{v}/k{k}": {"loop_ms": [], "gpu_ms": [], "frame_ms": []} for v, k in settings}
 ref = None
+mismatches = []
 for r in range(a.rounds):
     for v, k in settings:
         pt.set_kernel_variant(v)
@@ -47,7 +48,11 @@ for r in range(a.rounds):
         acc = pt.accum().view(np.uint32)
         if ref is None:
             ref = acc.copy()
-        assert np.array_equal(acc, ref), f"variant {v} strip {k} differs"
+        if not np.array_equal(acc, ref):
+            bad = np.argwhere((acc != ref).any(-1))
+            mismatches.append({"setting": f"{v}/k{k}", "round": r, "pixels": int(len(bad)),
+                               "first": [int(x) for x in bad[0]], "got": [float(x) for x in acc[tuple(bad[0])].view(np.float32)],
+                               "want": [float(x) for x in ref[tuple(bad[0])].view(np.float32)]})
         if a.frames:
             t0 = time.perf_counter()
             for f in range(a.frames):
@@ -61,7 +66,7 @@ for r in range(a.rounds):
     pt.set_rng_state(st)
     fused.append(pt.render_raw(cam, 8, a.spp // 8, True))
 out = {"image": f"{a.width}x{a.height}", "spp": a.spp, "calls": a.spp // 8, "fused_ms_median": float(np.median(fused)),
-       "settings": {}}
+       "bit_identical": not mismatches, "mismatches": mismatches[:8], "settings": {}}
 for key, d in res.items():
     m = float(np.median(d["loop_ms"]))
     out["settings"][key] = {"loop_ms_median": round(m, 2), "gpu_ms_median": round(float(np.median(d["gpu_ms"])), 2),
@@ -70,3 +75,5 @@ for key, d in res.items():
     if d["frame_ms"]:
         out["settings"][key]["frame_ms_median"] = round(float(np.median(d["frame_ms"])), 4)
 print(json.dumps(out))
+if mismatches:
+    sys.exit(3)
