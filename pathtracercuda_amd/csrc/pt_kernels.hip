@@ -717,10 +717,12 @@ PT_DEV bool walk_interior_quad(const float4* __restrict__ qnodes, uint2* stack, 
         const float lo1 = fr.both ? __builtin_fminf(fr.loNext, fr.loF) : fr.loNext;
         stack[64u * sp] = make_uint2(w1, __float_as_uint(lo1));
         sp += (intoNear && farOn) ? 1u : 0u;
-        // entry 2: the far child of the side descended into
+        // entry 2: the far child of the side descended into (none when nothing is descended into:
+        // on a pair visit whose half misses, `fr` is the disabled half and must push nothing)
+        const bool descend = intoNear || farOn;
         stack[64u * sp] = make_uint2(sd.wF, __float_as_uint(sd.loF));
-        sp += sd.both ? 1u : 0u;
-        if (intoNear || farOn) {
+        sp += (descend && sd.both) ? 1u : 0u;
+        if (descend) {
             cur = sd.wNext;
         } else {
             bool found = false;
