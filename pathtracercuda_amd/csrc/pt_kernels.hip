@@ -592,10 +592,18 @@ PT_DEV float slab_lo_x(const SlabRay& R, f2v bx, f2v by, f2v bz, float tMin, flo
 // the next node and of the pushed (far) child depends on the order: "both hit" and "any hit" are
 // symmetric, so the hit flags stay compare results (wave masks, combined on the SALU) and three
 // selects pick the next node, the far node and its entry distance.
+// t_max can RISE during a traversal: the sphere's far-root quirk (Hittable.inl:158, prim_hit_rec)
+// accepts t1 > t_max when t0 <= t_min, and the reference then tests the boxes it pops with that
+// larger t_max.  So a pending child may be dropped only for a reason that does not depend on t_max:
+// a far child is pushed when the near one is hit now and the far box meets the ray at all (X > lo);
+// whether it still passes is decided when it is popped (t_max > lo), as in trace.cu:48-98.
 struct ChildPair {
-    bool both, any;             // both children hit / at least one does
-    uint32_t wNext, wF;         // next node (the near one when both hit), far node (pushed when both hit)
+    bool push, any;             // push: the near child is hit and the far box meets the ray; any: a child is hit
+    uint32_t wNext, wF;         // next node (the near one when both hit), far node
     float loNext, loF;          // their slab entry distances
+    bool gBoth, gAny;           // both / any child box meets the ray (t_max-free: the 4-wide far side)
+    uint32_t wG;                // the one child that meets the ray when only one does
+    float loG, loMin;           // its lo; the smaller lo of the two
 };
 
 template <bool ALLFAST = false>
@@ -607,16 +615,22 @@ PT_DEV ChildPair cb_pair(const float4& Q0, const float4& Q1, const float4& Q2, c
     const float loR = slab_lo_x<ALLFAST>(R, f2(Q2.x, Q2.y), f2(Q2.z, Q2.w), f2(Q1.z, Q1.w), tMin, XR);
     const bool isNeg = (negMask & __float_as_uint(Q3.z)) != 0u;
     const uint32_t wL = __float_as_uint(Q3.x), wR = __float_as_uint(Q3.y);
-    const bool hL = XL > loL && tMax > loL;
-    const bool hR = XR > loR && tMax > loR;
+    const bool gL = XL > loL, gR = XR > loR;
+    const bool hL = gL && tMax > loL;
+    const bool hR = gR && tMax > loR;
     const bool takeL = hL && (!hR || !isNeg);
     ChildPair c;
-    c.both = hL && hR;
+    c.push = isNeg ? (hR && gL) : (hL && gR);
     c.any = hL || hR;
     c.wNext = takeL ? wL : wR;
     c.loNext = takeL ? loL : loR;
     c.wF = isNeg ? wL : wR;
     c.loF = isNeg ? loL : loR;
+    c.gBoth = gL && gR;
+    c.gAny = gL || gR;
+    c.wG = gL ? wL : wR;
+    c.loG = gL ? loL : loR;
+    c.loMin = __builtin_fminf(loL, loR);
     return c;
 }
 
@@ -634,7 +648,7 @@ PT_DEV ChildPair cb_children(const float4* __restrict__ cnodes, uint32_t cur, co
 // all its waves): ALLFAST (wave-uniform, decided by the caller) drops the per-lane exact-form
 // branch of the slab test, and the far child is written to the stack unconditionally -- the slot
 // above the top, inside the lane's column since an interior node has at most depth - 2 pending
-// entries -- with the stack pointer advanced only when both children are hit.
+// entries -- with the stack pointer advanced only when the far child is to be kept (ChildPair).
 template <bool STATS, bool ALLFAST>
 PT_DEV bool walk_interior(const float4* __restrict__ cnodes, uint2* stack, const SlabRay& R, uint32_t negMask,
                           float tMin, float tMax, uint32_t& cur, uint32_t& sp, Counters& cnt)
@@ -643,7 +657,7 @@ PT_DEV bool walk_interior(const float4* __restrict__ cnodes, uint2* stack, const
         if (STATS) { cnt.node_tests += 2; wave_tick(cnt.w_node); }
         const ChildPair ch = cb_children<ALLFAST>(cnodes, cur, R, negMask, tMin, tMax);
         stack[64u * sp] = make_uint2(ch.wF, __float_as_uint(ch.loF));
-        sp += ch.both ? 1u : 0u;
+        sp += ch.push ? 1u : 0u;
         if (ch.any) {
             cur = ch.wNext;
         } else {
@@ -679,13 +693,13 @@ PT_DEV bool walk_interior(const float4* __restrict__ cnodes, uint2* stack, const
 // monotonically; an infinite 1/d gives both boxes the same +-inf or no-constraint NaN bound) -- so
 // testing the near child's children directly gives the reference's verdicts (trace.cu:48-77: near
 // child tested at the same t_max, then its children at the same t_max).  The far side is pushed as
-// ONE entry, as the reference pushes the far child (trace.cu:75): if both of its children hit now,
-// a PAIR reference with lo = the smaller of their entry distances -- when popped with t_max <= lo
-// neither child can pass (t_max only falls), otherwise the pair is visited and both children are
-// re-tested with the then-current t_max, exactly the reference's visit of the far child (its own
-// box test implied by nesting); if one child hits, that child's word and lo, as a plain far entry;
-// if none, nothing (it fails at any later, smaller t_max).  A pair visit fetches the same record
-// and enables only its half.  Visit order, node culling and primitive tests per lane are the
+// ONE entry, as the reference pushes the far child (trace.cu:75), decided without t_max (which can
+// rise before the pop, ChildPair): if both of its child boxes meet the ray, a PAIR reference with
+// lo = the smaller of their entry distances -- popped with t_max <= lo neither child can pass,
+// otherwise the pair is visited and both children are tested with the then-current t_max, exactly
+// the reference's visit of the far child (its own box test implied by nesting); if one does, that
+// child's word and lo, as a plain far entry; if none, nothing (no t_max can make it pass).  A pair
+// visit fetches the same record and enables only its half.  Visit order, node culling and primitive tests per lane are the
 // reference's; the stack holds at most the reference's pending count (<= one entry per level).
 // ---------------------------------------------------------------------------------------------
 constexpr uint32_t kPairBit = 1u << 23;
@@ -708,20 +722,21 @@ PT_DEV bool walk_interior_quad(const float4* __restrict__ qnodes, uint2* stack, 
         const float4* qf = qnodes + 8 * r + 4 * (nearIsB ^ 1u);
         const ChildPair nr = cb_pair<ALLFAST>(qn[0], qn[1], qn[2], qn[3], R, negMask, tMin, tMax);
         const ChildPair fr = cb_pair<ALLFAST>(qf[0], qf[1], qf[2], qf[3], R, negMask, tMin, tMax);
-        const bool farOn = !isPair && fr.any;
         // descend into the near side if any of its children passes, else into the far side (same t_max)
         const bool intoNear = nr.any;
+        const bool farOn = !isPair && fr.any;
         const ChildPair& sd = intoNear ? nr : fr;
-        // entry 1: the far side, below the near side's far child (pushed only when descending near)
-        const uint32_t w1 = fr.both ? (kPairBit | (2u * r + (nearIsB ^ 1u))) : fr.wNext;
-        const float lo1 = fr.both ? __builtin_fminf(fr.loNext, fr.loF) : fr.loNext;
+        // entry 1: the far side, below the near side's far child, kept when descending near and any of
+        // its child boxes meets the ray (t_max-free, see ChildPair): a pair reference when both do
+        const uint32_t w1 = fr.gBoth ? (kPairBit | (2u * r + (nearIsB ^ 1u))) : fr.wG;
+        const float lo1 = fr.gBoth ? fr.loMin : fr.loG;
         stack[64u * sp] = make_uint2(w1, __float_as_uint(lo1));
-        sp += (intoNear && farOn) ? 1u : 0u;
+        sp += (intoNear && !isPair && fr.gAny) ? 1u : 0u;
         // entry 2: the far child of the side descended into (none when nothing is descended into:
         // on a pair visit whose half misses, `fr` is the disabled half and must push nothing)
         const bool descend = intoNear || farOn;
         stack[64u * sp] = make_uint2(sd.wF, __float_as_uint(sd.loF));
-        sp += (descend && sd.both) ? 1u : 0u;
+        sp += (descend && sd.push) ? 1u : 0u;
         if (descend) {
             cur = sd.wNext;
         } else {
@@ -774,7 +789,7 @@ PT_DEV uint32_t traverse_cb(const float4* __restrict__ cnodes, const float4* __r
         while ((cur >> 24) == 0u) {                               // interior walk
             if (STATS) { cnt.node_tests += 2; wave_tick(cnt.w_node); }
             const ChildPair ch = cb_children(cnodes, cur, R, negMask, tMin, tMax);   // trace.cu:66-77
-            if (ch.both) {
+            if (ch.push) {
                 stack[64u * sp] = make_uint2(ch.wF, __float_as_uint(ch.loF));
                 ++sp;
             }

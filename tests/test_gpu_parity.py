@@ -460,16 +460,18 @@ def test_full_frame_bitexact_and_nan_pixels(gpu_available, scenes):
     # against the oracle: every word, and the pixels poisoned by the reference's 0/0 VNDF pdf
     # (MonteCarlo.h:110-113; LAMBERT_GGX with VdotH clamped to 0) counted on both sides -- the one
     # full-frame statistic a change in the pdf path would move
+    # 96 spp (12 calls): rays whose t_max rises mid-traversal (the sphere's far-root quirk) are rare;
+    # round 4 found a walk that dropped pending boxes on them at the 11th call of this frame
     W, H = 1920, 1080
     pt, cam, ref, osc = pair(scenes / "generated_scene.scene.json", W, H)
-    pt.render(cam, 8, True, chunks=4)
-    ref.render(osc.camera, 8, True, chunks=4)
+    pt.render(cam, 8, True, chunks=12)
+    ref.render(osc.camera, 8, True, chunks=12)
     acc = pt.accum()
     nan_gpu = int((~np.isfinite(acc)).any(-1).sum())
     nan_ref = int((~np.isfinite(ref.accum)).any(-1).sum())
-    print(f"NaN pixels at 1080p x 32 spp: gpu {nan_gpu}, oracle {nan_ref}")
+    print(f"NaN pixels at 1080p x 96 spp: gpu {nan_gpu}, oracle {nan_ref}")
     assert nan_gpu == nan_ref
-    assert_bitexact(acc, ref.accum, "1080p full frame x 32 spp")
+    assert_bitexact(acc, ref.accum, "1080p full frame x 96 spp")
     assert np.array_equal(pt.rng_state(), ref.rng_array())
 
 
@@ -615,3 +617,25 @@ def test_strip_units_bitexact(gpu_available, scenes, W, H, band):
         if want is None:
             want = got
         assert np.array_equal(got[0], want[0]) and np.array_equal(got[1], want[1]), f"strip K={K}"
+
+
+def test_quad_walk_full_frame_matches(gpu_available, scenes):
+    # the 4-wide walks (variants 59/60/61/66/67) on the whole 1080p frame, several render() calls
+    # with history, against the 2-wide default: rare traversal paths (pair visits whose half misses,
+    # ties re-tested after a far side) show up only at this many rays
+    W, H = 1920, 1080
+    pt = pa.Pathtracer(W, H)
+    cam = pt.load_scene(scenes / "generated_scene.scene.json")
+    pt.set_strip_units(1)
+    st = pt.rng_state()
+    want = None
+    for variant in (40, 59, 60, 61, 66, 67):
+        pt.set_kernel_variant(variant)
+        pt.set_rng_state(st)
+        for i in range(16):
+            pt.render(cam, 8, i == 0)
+        got = pt.accum().view(np.uint32).copy()
+        if want is None:
+            want = got
+        diff = int((got != want).any(-1).sum())
+        assert diff == 0, f"variant {variant}: {diff} pixels differ from variant 40"

@@ -55,11 +55,18 @@ def lo_x(bmin, bmax, o, d):
     return lo, hi
 
 
+RISE = [False]
+
+
 def prim_stub(p, ray_id, tmax):
-    """Deterministic stand-in for Hittable::hit: hits 30 % of the time, at a t below t_max."""
+    """Deterministic stand-in for Hittable::hit: hits 30 % of the time, at a t below t_max -- or, with
+    RISE set, sometimes ABOVE t_max, as the sphere's far-root quirk does (Hittable.inl:158: t1 is
+    accepted when t0 <= t_min, whatever t_max is)."""
     h = (p * 2654435761 + ray_id * 40503) & 0xffffffff
     if h % 10 >= 3:
         return None
+    if RISE[0] and h % 5 == 0 and tmax < 1e30:
+        return F(float(tmax) * 1.5 + 0.5)
     t = F(T_MIN + (h >> 8) % 1000 / 1000.0 * min(float(tmax), 50.0))
     return t if T_MIN < t <= tmax else None
 
@@ -132,15 +139,21 @@ def build_quads(nodes):
 
 
 def cb_pair(half, o, d, negmask, tmax):
+    """pt_kernels.hip cb_pair: hit flags at t_max, and the t_max-free 'box meets the ray' flags that
+    decide what is kept for later."""
     (lb, rb, wl, wr, axis) = half
     lol, xl = lo_x(*lb, o, d)
     lor, xr = lo_x(*rb, o, d)
     isneg = (negmask & axis) != 0
-    hl = xl > lol and tmax > lol
-    hr = xr > lor and tmax > lor
+    gl, gr = xl > lol, xr > lor
+    hl = gl and tmax > lol
+    hr = gr and tmax > lor
     takel = hl and (not hr or not isneg)
-    return {"both": hl and hr, "any": hl or hr, "wNext": wl if takel else wr, "loNext": lol if takel else lor,
-            "wF": wl if isneg else wr, "loF": lol if isneg else lor}
+    return {"push": (hr and gl) if isneg else (hl and gr), "any": hl or hr,
+            "wNext": wl if takel else wr, "loNext": lol if takel else lor,
+            "wF": wl if isneg else wr, "loF": lol if isneg else lor,
+            "gBoth": gl and gr, "gAny": gl or gr, "wG": wl if gl else wr, "loG": lol if gl else lor,
+            "loMin": min(lol, lor)}
 
 
 def quad_walk(recs, root_word, root_box, nodes, o, d, ray_id):
@@ -168,18 +181,18 @@ def quad_walk(recs, root_word, root_box, nodes, o, d, ray_id):
             nr, fr = (hb, ha) if near_b else (ha, hb)
             far_on = not pair and fr["any"]
             if nr["any"]:
-                if far_on:
-                    if fr["both"]:
-                        stack.append((PAIR | (2 * r + (0 if near_b else 1)), min(fr["loNext"], fr["loF"])))
+                if not pair and fr["gAny"]:
+                    if fr["gBoth"]:
+                        stack.append((PAIR | (2 * r + (0 if near_b else 1)), fr["loMin"]))
                     else:
-                        stack.append((fr["wNext"], fr["loNext"]))
+                        stack.append((fr["wG"], fr["loG"]))
                 sd = nr
             elif far_on:
                 sd = fr
             else:
                 cur = pop()
                 continue
-            if sd["both"]:
+            if sd["push"]:
                 stack.append((sd["wF"], sd["loF"]))
             cur = sd["wNext"]
         else:
@@ -196,6 +209,7 @@ def quad_walk(recs, root_word, root_box, nodes, o, d, ray_id):
 def rays(nodes, n, seed):
     rng = np.random.default_rng(seed)
     bmin, bmax = box(nodes[0])
+    leaves = [m for m in nodes if m.primitive_count_axis >> 16]
     out = []
     for k in range(n):
         o = (bmin + (bmax - bmin) * rng.uniform(-0.2, 1.2, 3)).astype(F)
@@ -205,9 +219,69 @@ def rays(nodes, n, seed):
         if k % 7 == 2:                       # origin on a box face of a random node
             m = nodes[rng.integers(len(nodes))]
             o[k % 3] = np.array(m.aabb_min, F)[k % 3]
+        if k % 2 == 0:                       # aimed at a random leaf's box: rays that reach primitives
+            leaf = leaves[rng.integers(len(leaves))]
+            lmin, lmax = box(leaf)
+            d = (lmin + (lmax - lmin) * rng.uniform(0, 1, 3) - o).astype(F)
         d = (d / np.linalg.norm(d)).astype(F) if np.linalg.norm(d) > 0 else np.array([0, 1, 0], F)
         out.append((o, d))
     return out
+
+
+def cb_walk(nodes, o, d, ray_id):
+    """The 2-wide child-box walk (walk_interior / traverse_cb): both children tested at the parent's
+    visit, the far child kept by cb_pair's `push` and re-tested (t_max > lo) when popped."""
+    negmask = (d[0] < 0) | ((d[1] < 0) << 1) | ((d[2] < 0) << 2)
+    tests, stack, tmax = [], [], F(np.finfo(np.float32).max)
+    lo0, x0 = lo_x(*box(nodes[0]), o, d)
+    if not (x0 > lo0 and tmax > lo0):
+        return tests
+    cur = 0
+
+    def pop():
+        while stack:
+            w, lo = stack.pop()
+            if tmax > lo:
+                return w
+        return None
+
+    while cur is not None:
+        n = nodes[cur]
+        cnt = n.primitive_count_axis >> 16
+        if cnt:
+            for i in range(cnt):
+                tests.append(n.offset + i)
+                t = prim_stub(n.offset + i, ray_id, tmax)
+                if t is not None:
+                    tmax = t
+            cur = pop()
+            continue
+        a, b = cur + 1, n.offset
+        ch = cb_pair((box(nodes[a]), box(nodes[b]), a, b, 1 << ((n.primitive_count_axis >> 8) & 0xff)), o, d, negmask,
+                     tmax)
+        if ch["push"]:
+            stack.append((ch["wF"], ch["loF"]))
+        cur = ch["wNext"] if ch["any"] else pop()
+    return tests
+
+
+@pytest.mark.parametrize("rise", [False, True])
+@pytest.mark.parametrize("scene,nrays", [("generated_scene", 1500), ("cornell_box", 800), ("test_shapes", 400)])
+def test_child_box_walks_match_reference_order(scene, nrays, rise):
+    """Both shipped walks (2-wide and 4-wide) against hitBVH, also when t_max rises mid-traversal
+    (the sphere's far-root quirk): pending children are dropped only for t_max-free reasons."""
+    RISE[0] = rise
+    try:
+        root = pathlib.Path(__file__).resolve().parents[1]
+        sc = pa.Scene(str(root / "scenes" / f"{scene}.scene.json"), 64, 64)
+        nodes = list(sc.bvh()[0])
+        recs, root_word = build_quads(nodes)
+        for k, (o, d) in enumerate(rays(nodes, nrays, 11)):
+            want = reference_walk(nodes, o, d, k)
+            assert cb_walk(nodes, o, d, k) == want, ("2-wide", k)
+            assert quad_walk(recs, root_word, box(nodes[0]), nodes, o, d, k) == want, ("4-wide", k)
+    finally:
+        RISE[0] = False
 
 
 @pytest.mark.parametrize("scene,nrays", [("generated_scene", 1500), ("cornell_box", 800), ("test_shapes", 400)])
