@@ -236,7 +236,7 @@ PT_API int pt_set_issue_priority(pt_context *ctx, int mode, uint32_t level3, uin
  * the remaining dead ends run as a plain resume launch (default 6; 0 exercises the resume path). */
 /* Tuning knob: tiles per dispatch unit of launches with few samples per pixel (a row strip of K
  * tiles; a lane whose pixel is done takes the same position in the next tile of its strip).
- * 0 = automatic (K = 2 at <= 64 samples per pixel on large images), 1 = off, K = 2..16 = always K
+ * 0 = automatic (K = 4 at <= 2 samples per pixel on large images), 1 = off, K = 2..16 = always K
  * (resumable variants).  Results are identical for every setting. */
 PT_API int pt_set_strip_units(pt_context *ctx, int mode);
 PT_API int pt_set_sample_groups(pt_context *ctx, int mode);

@@ -23,6 +23,7 @@
 #include <rocprim/device/device_radix_sort.hpp>
 #include <rccl/rccl.h>
 #include <stdint.h>
+#include <cmath>
 #include <string.h>
 #include <stdio.h>
 #include <string>
@@ -110,6 +111,7 @@ struct TraceParams {
     uint32_t occCap;            // host only: persistent grids hold at most this many workgroups per CU (0 = all)
     uint32_t prio[3];           // issue priority by order position: < prio[0] -> 3, < prio[1] -> 2, < prio[2] -> 1
     uint32_t strip;             // MODE 3: tiles per dispatch unit (a row strip of `strip` tiles; see trace_kernel)
+    uint32_t camRise;           // the camera lies in or near a sphere (primary rays: SlabRay::rise)
 };
 
 // Speculative sample groups: window of a group's start offset in which an earlier group's parse can
@@ -558,6 +560,7 @@ struct SlabRay {
     f3 o;
     float ix, iy, iz;
     bool fast;
+    bool rise;                  // t_max may rise on this ray (its origin may lie in or near a sphere, ChildPair)
 };
 
 // lo and X of one box (see above); the fast form under the same conditions as node_test_fast.
@@ -594,9 +597,12 @@ PT_DEV float slab_lo_x(const SlabRay& R, f2v bx, f2v by, f2v bz, float tMin, flo
 // selects pick the next node, the far node and its entry distance.
 // t_max can RISE during a traversal: the sphere's far-root quirk (Hittable.inl:158, prim_hit_rec)
 // accepts t1 > t_max when t0 <= t_min, and the reference then tests the boxes it pops with that
-// larger t_max.  So a pending child may be dropped only for a reason that does not depend on t_max:
-// a far child is pushed when the near one is hit now and the far box meets the ray at all (X > lo);
-// whether it still passes is decided when it is popped (t_max > lo), as in trace.cu:48-98.
+// larger t_max.  A far child that fails its test now would pass it later, so on such a ray a pending
+// child may be dropped only for a reason that does not depend on t_max: the far child is pushed when
+// the near one is hit now and the far box meets the ray at all (X > lo), and whether it still passes
+// is decided when it is popped (t_max > lo), as in trace.cu:48-98.  t0 <= t_min needs the ray origin
+// inside a sphere or within t_min of it; rays whose origin cannot be (SlabRay::rise false, decided per
+// primitive and camera on the host, pt_set_scene / render_impl) keep a far child only if it is hit now.
 struct ChildPair {
     bool push, any;             // push: the near child is hit and the far box meets the ray; any: a child is hit
     uint32_t wNext, wF;         // next node (the near one when both hit), far node
@@ -615,9 +621,9 @@ PT_DEV ChildPair cb_pair(const float4& Q0, const float4& Q1, const float4& Q2, c
     const float loR = slab_lo_x<ALLFAST>(R, f2(Q2.x, Q2.y), f2(Q2.z, Q2.w), f2(Q1.z, Q1.w), tMin, XR);
     const bool isNeg = (negMask & __float_as_uint(Q3.z)) != 0u;
     const uint32_t wL = __float_as_uint(Q3.x), wR = __float_as_uint(Q3.y);
-    const bool gL = XL > loL, gR = XR > loR;
-    const bool hL = gL && tMax > loL;
-    const bool hR = gR && tMax > loR;
+    const bool hL = XL > loL && tMax > loL;
+    const bool hR = XR > loR && tMax > loR;
+    const bool gL = R.rise ? XL > loL : hL, gR = R.rise ? XR > loR : hR;   // kept for later
     const bool takeL = hL && (!hR || !isNeg);
     ChildPair c;
     c.push = isNeg ? (hR && gL) : (hL && gR);
@@ -753,11 +759,12 @@ PT_DEV bool walk_interior_quad(const float4* __restrict__ qnodes, uint2* stack, 
 
 template <bool STATS>
 PT_DEV uint32_t traverse_cb(const float4* __restrict__ cnodes, const float4* __restrict__ prims, uint2* stack,
-                            const TraceParams& P, f3 o, f3 d, float& tHit, Counters& cnt)
+                            const TraceParams& P, f3 o, f3 d, bool rise, float& tHit, Counters& cnt)
 {
     const float tMin = 0.001f;
     float tMax = kFltMax;
     SlabRay R;
+    R.rise = rise;
     R.o = o;
     R.ix = rcp_rn(d.x);
     R.iy = rcp_rn(d.y);
@@ -838,10 +845,11 @@ struct TravState {
 // far-child write).  WW = 200 + EXITQ selects this traversal.
 template <bool STATS, int EXITQ, bool QUAD = false>
 PT_DEV bool traverse_cb_phase(const float4* __restrict__ cnodes, const float4* __restrict__ prims, uint2* stack,
-                              const TraceParams& P, f3 o, f3 d, bool fresh, TravState& ts, Counters& cnt)
+                              const TraceParams& P, f3 o, f3 d, bool rise, bool fresh, TravState& ts, Counters& cnt)
 {
     const float tMin = 0.001f;
     SlabRay R;
+    R.rise = rise;
     R.o = o;
     R.ix = rcp_rn(d.x);
     R.iy = rcp_rn(d.y);
@@ -1042,6 +1050,7 @@ struct PathState {
                       // (x, y, z at lds_f()[acc], [acc + 64], [acc + 128])
     uint32_t s, c, bounce;
     bool alive;
+    bool rise;        // the current ray's origin may lie in or near a sphere (ChildPair; host flags)
 };
 
 // camera ray of one sample (trace.cu:190-192, Camera.inl:25-28): two uniforms, x then y
@@ -1081,7 +1090,8 @@ PT_DEV bool shade(const TraceParams& P, const float4* __restrict__ prims, uint32
     const float4 q0 = prims[4 * e + 0];
     const float4 q1 = prims[4 * e + 1];
     const float4 q2 = prims[4 * e + 2];
-    const uint32_t ptype = __float_as_uint(prims[4 * e + 3].x);
+    const float4 pw = prims[4 * e + 3];
+    const uint32_t ptype = __float_as_uint(pw.x);
     ps.L = add(ps.L, mul(ps.T, mk(m1.x, m1.y, m1.z)));                      // trace.cu:139
     if (ps.bounce == 4) {
         // 5th segment: its scattered ray is discarded (trace.cu:109); only the two uniforms of
@@ -1162,6 +1172,10 @@ PT_DEV bool shade(const TraceParams& P, const float4* __restrict__ prims, uint32
     ps.T = mul(ps.T, w);
     ps.o = sf.p;
     ps.d = sd;
+    // the new ray starts on primitive e: it may start in or near a sphere if e's box meets a
+    // sphere's (host flag), or if e is a sphere this path was inside of (a ray leaving a sphere it hit
+    // from outside points outward, the sampled direction lies in the face-forward hemisphere)
+    ps.rise = (__float_as_uint(pw.y) & 1u) != 0u || (ps.rise && ptype == SPHERE);
     ++ps.bounce;
     return false;
 }
@@ -1190,6 +1204,7 @@ PT_DEV void finish_path(const TraceParams& P, PathState& ps, Xorwow& rng, float 
     }
     if (ps.alive) {
         camera_ray(P, fx, fy, rng, ps.o, ps.d);
+        ps.rise = P.camRise != 0u;
         ps.L = splat(0.0f);
         ps.T = splat(1.0f);
         ps.bounce = 0;
@@ -1391,6 +1406,7 @@ PT_DEV void ssg_finish(const TraceParams& P, PathState& ps, Xorwow& rng, float f
         return;
     }
     camera_ray(P, fx, fy, rng, ps.o, ps.d);
+    ps.rise = P.camRise != 0u;
     ps.L = splat(0.0f);
     ps.T = splat(1.0f);
     ps.bounce = 0;
@@ -1548,6 +1564,7 @@ __global__ void __launch_bounds__(WPB * 64, MINW) trace_kernel(TraceParams P)
         else load_pixel<AUX>(P, pc, rng, ps, accL);
         float fx = (float)(int32_t)pc.px, fy = (float)(int32_t)pc.py;
         camera_ray(P, fx, fy, rng, ps.o, ps.d);
+        ps.rise = P.camRise != 0u;
         uint32_t stripK = 0;                     // STRIP: this lane's tile within the unit
         uint64_t tAll = STATS ? __builtin_amdgcn_s_memtime() : 0;
         uint64_t tDone = 0;
@@ -1568,7 +1585,7 @@ __global__ void __launch_bounds__(WPB * 64, MINW) trace_kernel(TraceParams P)
                 bool tdone = true;
                 if (!held) {
                     tdone = traverse_cb_phase<STATS, WW % 100, QUAD>(nodes, prims, reinterpret_cast<uint2*>(stack), P,
-                                                                ps.o, ps.d, fresh, ts, cnt);
+                                                                ps.o, ps.d, ps.rise, fresh, ts, cnt);
                     fresh = tdone;
                 }
                 if (DEFERQ > 0 || SKYQ > 0) {
@@ -1602,6 +1619,7 @@ __global__ void __launch_bounds__(WPB * 64, MINW) trace_kernel(TraceParams P)
                             fx = (float)(int32_t)pc.px;
                             fy = (float)(int32_t)pc.py;
                             camera_ray(P, fx, fy, rng, ps.o, ps.d);
+                            ps.rise = P.camRise != 0u;
                         }
                     }
                 }
@@ -1612,7 +1630,7 @@ __global__ void __launch_bounds__(WPB * 64, MINW) trace_kernel(TraceParams P)
         while (WW < 100 && ps.alive) {
             if (STATS) { cnt.segments++; wave_tick(cnt.w_segments); }
             float t;
-            const uint32_t e = WW >= 3 ? traverse_cb<STATS>(nodes, prims, reinterpret_cast<uint2*>(stack), P, ps.o, ps.d, t, cnt)
+            const uint32_t e = WW >= 3 ? traverse_cb<STATS>(nodes, prims, reinterpret_cast<uint2*>(stack), P, ps.o, ps.d, ps.rise, t, cnt)
                                        : traverse<STATS, WW>(nodes, prims, stack, ps.o, ps.d, P.slabFast != 0, t, cnt);
             uint64_t tS = STATS ? __builtin_amdgcn_s_memtime() : 0;
             if (shade<STATS>(P, prims, e, t, ps, rng, cnt)) {
@@ -2044,6 +2062,7 @@ struct pt_context {
     float4* mats = nullptr;
     float4* cnodes = nullptr;   // child-box records (traverse_cb); null when the scene exceeds its encoding
     uint32_t cnodeCount = 0, rootWord = 0;
+    std::vector<double> sphereBoxes;  // per sphere: world box grown by the rising-t_max margin (pt_set_scene)
     float4* qnodes = nullptr;   // 4-wide child-box records (walk_interior_quad); null when boxes are not nested
     uint32_t qnodeCount = 0, qrootWord = 0, qstackDepth = 1;
     float rootBox[6] = {};
@@ -2268,12 +2287,14 @@ static hipError_t launch_strip(int v, const TraceParams& P, hipStream_t stream)
 
 static bool strip_capable(int v) { return v == 40 || v == 41 || v == 46 || v == 60 || v == 61 || v == 66; }
 
-// Tiles per dispatch unit.  A launch of few samples per pixel (the reference's 8-spp render() calls,
-// 1-spp progressive frames) idles the lanes whose pixels finish first for the rest of their tile
-// (23 % of lane time at 8 spp against 6 % at 1024); strips of K tiles let those lanes
-// go on with the next tile.  Automatic: K = 2 for launches of at most 64 samples per pixel that
-// keep at least ~3 units per wave slot; the variant must be a strip-capable one.
-constexpr uint64_t kStripMaxSamples = 64;
+// Tiles per dispatch unit.  A launch of few samples per pixel idles the lanes whose pixels finish
+// first for the rest of their tile; strips of K tiles let those lanes go on with the next tile.
+// Measured at 1080p (tools/call_loop.py, profiles/r04_call_loop.json): 1-spp progressive frames
+// 0.673 -> 0.646 ms (K = 2) -> 0.592 ms (K = 4); the reference's 8-spp calls 316 -> 320 ms (K = 2)
+// -> 466 ms (K = 4) per 128 calls -- units of several tiles are too few to balance the launch's tail
+// there.  Automatic: K = 4 for launches of at most 2 samples per pixel with at least ~6 tiles per
+// wave slot; the variant must be a strip-capable one.
+constexpr uint64_t kStripMaxSamples = 2;
 
 static uint32_t strip_tiles(const pt_context* ctx, int variant, uint32_t tiles, uint64_t samples)
 {
@@ -2285,7 +2306,7 @@ static uint32_t strip_tiles(const pt_context* ctx, int variant, uint32_t tiles, 
     int cus = 0;
     if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, ctx->device) != hipSuccess) return 1;
     const uint64_t slots = (uint64_t)cus * 4 * 5;
-    return (uint64_t)tiles >= 6 * slots ? 2u : 1u;
+    return (uint64_t)tiles >= 6 * slots ? 4u : 1u;
 }
 
 static bool variant_shipped(int v)
@@ -2584,13 +2605,83 @@ PT_API int pt_set_scene(pt_context* ctx, const pt_bvh_node* nodes, uint32_t node
             q[3] = make_float4(u2f(leaf ? qword(c) : qword(c + 1)), u2f(wR), u2f(axisBit), 0.0f);
         }
     }
+    // Rising t_max (ChildPair): a ray can meet a sphere with t0 <= t_min only if its origin lies in
+    // the sphere or within t_min of it.  Origins lie on primitives (and at the camera, render_impl),
+    // so primitive i is flagged (hp[4 i + 3].y bit 0) when its box meets the box of another sphere
+    // grown by a margin (t_min + rounding of hit points).  Boxes: every shape lies in [-1, 1]^3 of its
+    // object space (Hittable.inl), so the world box is center + |M| * (1, 1, 1) with M the inverse of
+    // the 3x3 part of inv_transform_rows; computed in double and grown by a relative 1e-4.
+    std::vector<double> box(6 * (size_t)prim_count);
+    std::vector<uint32_t> spheres;
+    for (uint32_t i = 0; i < prim_count; ++i) {
+        const float(&A)[3][4] = prims[i].inv_transform_rows;
+        double a[3][3], m[3][3];
+        for (int r = 0; r < 3; ++r)
+            for (int c = 0; c < 3; ++c) a[r][c] = A[r][c];
+        const double det = a[0][0] * (a[1][1] * a[2][2] - a[1][2] * a[2][1]) - a[0][1] * (a[1][0] * a[2][2] - a[1][2] * a[2][0]) +
+                           a[0][2] * (a[1][0] * a[2][1] - a[1][1] * a[2][0]);
+        double* b = &box[6 * (size_t)i];
+        if (!(std::fabs(det) > 0.0) || !std::isfinite(det)) {   // degenerate: unbounded, flag everything
+            for (int k = 0; k < 3; ++k) { b[k] = -HUGE_VAL; b[3 + k] = HUGE_VAL; }
+        } else {
+            for (int r = 0; r < 3; ++r)
+                for (int c = 0; c < 3; ++c)
+                    m[r][c] = (a[(c + 1) % 3][(r + 1) % 3] * a[(c + 2) % 3][(r + 2) % 3] -
+                               a[(c + 1) % 3][(r + 2) % 3] * a[(c + 2) % 3][(r + 1) % 3]) / det;
+            for (int k = 0; k < 3; ++k) {
+                const double ctr = -(m[k][0] * A[0][3] + m[k][1] * A[1][3] + m[k][2] * A[2][3]);
+                const double ext = std::fabs(m[k][0]) + std::fabs(m[k][1]) + std::fabs(m[k][2]);
+                const double pad = 1e-4 * (std::fabs(ctr) + ext) + 1e-6;
+                b[k] = ctr - ext - pad;
+                b[3 + k] = ctr + ext + pad;
+            }
+        }
+        if (prims[i].type == SPHERE) spheres.push_back(i);
+    }
+    std::vector<uint32_t> riseFlag(prim_count, 0u);
+    ctx->sphereBoxes.clear();
+    {
+        const double margin = 0.01;             // > t_min (0.001) with room for rounding
+        for (const uint32_t si : spheres) {
+            const double* sb = &box[6 * (size_t)si];
+            for (int k = 0; k < 6; ++k) ctx->sphereBoxes.push_back(sb[k] + (k < 3 ? -margin : margin));
+        }
+        // per sphere, the primitives whose boxes meet its grown box, found through the BVH (its node
+        // boxes bound the primitives' geometry)
+        std::vector<uint32_t> st;
+        for (size_t j = 0; j < spheres.size(); ++j) {
+            const double* sb = &ctx->sphereBoxes[6 * j];
+            st.assign(1, 0u);
+            while (!st.empty()) {
+                const uint32_t n = st.back();
+                st.pop_back();
+                const pt_bvh_node& nd = nodes[n];
+                bool meet = true;
+                for (int k = 0; k < 3; ++k) meet = meet && nd.aabb_min[k] <= sb[3 + k] && nd.aabb_max[k] >= sb[k];
+                if (!meet) continue;
+                const uint32_t count = nd.primitive_count_axis >> 16;
+                if (count == 0) {
+                    st.push_back(n + 1);
+                    st.push_back(nd.offset);
+                    continue;
+                }
+                for (uint32_t i = nd.offset; i < nd.offset + count; ++i) {
+                    if (i == spheres[j] || riseFlag[i]) continue;
+                    const double* b = &box[6 * (size_t)i];
+                    bool m2 = true;
+                    for (int k = 0; k < 3; ++k) m2 = m2 && b[k] <= sb[3 + k] && b[3 + k] >= sb[k];
+                    if (m2) riseFlag[i] = 1u;
+                }
+            }
+        }
+    }
     for (uint32_t i = 0; i < prim_count; ++i) {
         const pt_hittable& h = prims[i];
         const float(&R)[3][4] = h.inv_transform_rows;
         hp[4 * i + 0] = make_float4(R[0][0], R[1][0], R[0][1], R[1][1]);
         hp[4 * i + 1] = make_float4(R[0][2], R[1][2], R[0][3], R[1][3]);
         hp[4 * i + 2] = make_float4(R[2][0], R[2][1], R[2][2], R[2][3]);
-        hp[4 * i + 3] = make_float4(u2f(h.type), 0.0f, 0.0f, 0.0f);
+        hp[4 * i + 3] = make_float4(u2f(h.type), u2f(riseFlag[i]), 0.0f, 0.0f);
         hm[3 * i] = make_float4(h.base_color[0], h.base_color[1], h.base_color[2], h.roughness);
         hm[3 * i + 1] = make_float4(h.emissive[0], h.emissive[1], h.emissive[2], h.metalness);
         hm[3 * i + 2] = make_float4(u2f(h.texture_index), u2f(h.material_type), 0.0f, 0.0f);
@@ -2972,6 +3063,13 @@ static int render_impl(pt_context* ctx, const pt_camera* cam, uint32_t spp, uint
     P.cam.llc = hf3(cam->lower_left_corner);
     P.cam.horizontal = hf3(cam->horizontal);
     P.cam.vertical = hf3(cam->vertical);
+    // primary rays start at the camera: in or near a sphere's box -> their t_max may rise (ChildPair)
+    for (size_t j = 0; 6 * j < ctx->sphereBoxes.size() && !P.camRise; ++j) {
+        const double* sb = &ctx->sphereBoxes[6 * j];
+        bool in = true;
+        for (int k = 0; k < 3; ++k) in = in && cam->origin[k] >= sb[k] && cam->origin[k] <= sb[3 + k];
+        P.camRise = in ? 1u : 0u;
+    }
     P.nodeCount = ctx->nodeCount;
     P.primCount = ctx->primCount;
     P.stackDepth = ctx->stackDepth;

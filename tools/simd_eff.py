@@ -40,4 +40,4 @@ for v in [int(x) for x in a.variants.split(",")]:
               "lane_idle_after_pixel_done": round(st["cycles_lane_idle"] / (64.0 * tot), 3),
               "lane_utilisation": lane_utilisation(st)}
 print(json.dumps({"scene": pathlib.Path(a.scene).name, "image": f"{a.width}x{a.height}", "spp": a.spp * a.chunks,
-                  "variants": res}, indent=1))
+                  "variants": res}))
