@@ -1172,10 +1172,10 @@ PT_DEV bool shade(const TraceParams& P, const float4* __restrict__ prims, uint32
     ps.T = mul(ps.T, w);
     ps.o = sf.p;
     ps.d = sd;
-    // the new ray starts on primitive e: it may start in or near a sphere if e's box meets a
-    // sphere's (host flag), or if e is a sphere this path was inside of (a ray leaving a sphere it hit
-    // from outside points outward, the sampled direction lies in the face-forward hemisphere)
-    ps.rise = (__float_as_uint(pw.y) & 1u) != 0u || (ps.rise && ptype == SPHERE);
+    // the new ray starts on primitive e: it may start in or near a sphere if e's box meets another
+    // sphere's (host flag), or if e is a sphere -- its rounded hit point may lie inside it, and a
+    // grazing ray from there meets its far side beyond t_min on a large sphere
+    ps.rise = (__float_as_uint(pw.y) & 1u) != 0u || ptype == SPHERE;
     ++ps.bounce;
     return false;
 }
