@@ -112,6 +112,7 @@ struct TraceParams {
     uint32_t prio[3];           // issue priority by order position: < prio[0] -> 3, < prio[1] -> 2, < prio[2] -> 1
     uint32_t strip;             // MODE 3: tiles per dispatch unit (a row strip of `strip` tiles; see trace_kernel)
     uint32_t camRise;           // the camera lies in or near a sphere (primary rays: SlabRay::rise)
+    uint32_t riseAll;           // check mode (pt_set_rise_check): every ray keeps far children for a later test
 };
 
 // Speculative sample groups: window of a group's start offset in which an earlier group's parse can
@@ -1175,7 +1176,7 @@ PT_DEV bool shade(const TraceParams& P, const float4* __restrict__ prims, uint32
     // the new ray starts on primitive e: it may start in or near a sphere if e's box meets another
     // sphere's (host flag), or if e is a sphere -- its rounded hit point may lie inside it, and a
     // grazing ray from there meets its far side beyond t_min on a large sphere
-    ps.rise = (__float_as_uint(pw.y) & 1u) != 0u || ptype == SPHERE;
+    ps.rise = (__float_as_uint(pw.y) & 1u) != 0u || ptype == SPHERE || P.riseAll != 0u;
     ++ps.bounce;
     return false;
 }
@@ -2063,6 +2064,7 @@ struct pt_context {
     float4* cnodes = nullptr;   // child-box records (traverse_cb); null when the scene exceeds its encoding
     uint32_t cnodeCount = 0, rootWord = 0;
     std::vector<double> sphereBoxes;  // per sphere: world box grown by the rising-t_max margin (pt_set_scene)
+    bool riseAll = false;             // pt_set_rise_check
     float4* qnodes = nullptr;   // 4-wide child-box records (walk_interior_quad); null when boxes are not nested
     uint32_t qnodeCount = 0, qrootWord = 0, qstackDepth = 1;
     float rootBox[6] = {};
@@ -3064,6 +3066,8 @@ static int render_impl(pt_context* ctx, const pt_camera* cam, uint32_t spp, uint
     P.cam.horizontal = hf3(cam->horizontal);
     P.cam.vertical = hf3(cam->vertical);
     // primary rays start at the camera: in or near a sphere's box -> their t_max may rise (ChildPair)
+    P.riseAll = ctx->riseAll ? 1u : 0u;
+    P.camRise = P.riseAll;
     for (size_t j = 0; 6 * j < ctx->sphereBoxes.size() && !P.camRise; ++j) {
         const double* sb = &ctx->sphereBoxes[6 * j];
         bool in = true;
@@ -3287,6 +3291,13 @@ static int render_impl(pt_context* ctx, const pt_camera* cam, uint32_t spp, uint
         stats->leaf_pairs = h[20];
         stats->family_execs_compacted_in_round = h[21];
     }
+    return PT_OK;
+}
+
+PT_API int pt_set_rise_check(pt_context* ctx, int all_rays)
+{
+    if (!ctx || all_rays < 0 || all_rays > 1) return PT_ERR_ARG;
+    ctx->riseAll = all_rays != 0;
     return PT_OK;
 }
 

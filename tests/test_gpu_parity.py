@@ -639,3 +639,24 @@ def test_quad_walk_full_frame_matches(gpu_available, scenes):
             want = got
         diff = int((got != want).any(-1).sum())
         assert diff == 0, f"variant {variant}: {diff} pixels differ from variant 40"
+
+
+@pytest.mark.parametrize("scene,W,H,calls", [("generated_scene", 1920, 1080, 16), ("test_shapes", 640, 400, 16),
+                                              ("cornell_box", 512, 512, 16)])
+def test_rise_flags_cover_every_rising_ray(gpu_available, scenes, scene, W, H, calls):
+    # t_max rises only on rays that meet a sphere with t0 <= t_min; the host flags the rays that may
+    # (origin on a primitive whose box meets a sphere's, on a sphere, or at a camera inside one) and
+    # only those keep far children for a test at pop time.  With every ray following that rule (the
+    # reference's own) the bits must not change: a rising ray the flags missed would lose a box.
+    pt = pa.Pathtracer(W, H)
+    cam = pt.load_scene(scenes / f"{scene}.scene.json")
+    st = pt.rng_state()
+    out = []
+    for all_rays in (False, True):
+        pt.set_rise_check(all_rays)
+        pt.set_rng_state(st)
+        for i in range(calls):
+            pt.render(cam, 8, i == 0)
+        out.append(pt.accum().view(np.uint32).copy())
+    diff = int((out[0] != out[1]).any(-1).sum())
+    assert diff == 0, f"{scene}: {diff} pixels differ with every ray checked"
