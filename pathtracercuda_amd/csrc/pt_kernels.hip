@@ -624,7 +624,7 @@ PT_DEV ChildPair cb_pair(const float4& Q0, const float4& Q1, const float4& Q2, c
     const uint32_t wL = __float_as_uint(Q3.x), wR = __float_as_uint(Q3.y);
     const bool hL = XL > loL && tMax > loL;
     const bool hR = XR > loR && tMax > loR;
-    const bool gL = R.rise ? XL > loL : hL, gR = R.rise ? XR > loR : hR;   // kept for later
+    const bool gL = XL > loL && (R.rise || tMax > loL), gR = XR > loR && (R.rise || tMax > loR);   // kept for later
     const bool takeL = hL && (!hR || !isNeg);
     ChildPair c;
     c.push = isNeg ? (hR && gL) : (hL && gR);
@@ -1049,10 +1049,12 @@ struct PathState {
     f3 color;         // sum of the finished paths of the current render() call (trace.cu:186)
     uint32_t acc;     // float index of this lane's running accumulation value in the dynamic LDS
                       // (x, y, z at lds_f()[acc], [acc + 64], [acc + 128])
-    uint32_t s, c, bounce;
+    uint32_t s, c;
+    uint32_t bounce;  // segments of this path so far (bits 0-15) | kRiseBit: the current ray's origin
+                      // may lie in or near a sphere (ChildPair, host flags), kept in the same register
     bool alive;
-    bool rise;        // the current ray's origin may lie in or near a sphere (ChildPair; host flags)
 };
+constexpr uint32_t kRiseBit = 1u << 16;
 
 // camera ray of one sample (trace.cu:190-192, Camera.inl:25-28): two uniforms, x then y
 PT_DEV void camera_ray(const TraceParams& P, float fx, float fy, Xorwow& rng, f3& o, f3& d)
@@ -1091,10 +1093,9 @@ PT_DEV bool shade(const TraceParams& P, const float4* __restrict__ prims, uint32
     const float4 q0 = prims[4 * e + 0];
     const float4 q1 = prims[4 * e + 1];
     const float4 q2 = prims[4 * e + 2];
-    const float4 pw = prims[4 * e + 3];
-    const uint32_t ptype = __float_as_uint(pw.x);
+    const uint32_t ptype = __float_as_uint(prims[4 * e + 3].x);
     ps.L = add(ps.L, mul(ps.T, mk(m1.x, m1.y, m1.z)));                      // trace.cu:139
-    if (ps.bounce == 4) {
+    if ((ps.bounce & 0xffffu) == 4) {
         // 5th segment: its scattered ray is discarded (trace.cu:109); only the two uniforms of
         // Material.inl:40-41 are observable.
         (void)uniform(rng);
@@ -1176,8 +1177,8 @@ PT_DEV bool shade(const TraceParams& P, const float4* __restrict__ prims, uint32
     // the new ray starts on primitive e: it may start in or near a sphere if e's box meets another
     // sphere's (host flag), or if e is a sphere -- its rounded hit point may lie inside it, and a
     // grazing ray from there meets its far side beyond t_min on a large sphere
-    ps.rise = (__float_as_uint(pw.y) & 1u) != 0u || ptype == SPHERE || P.riseAll != 0u;
-    ++ps.bounce;
+    const bool rise = (__float_as_uint(m2.z) & 1u) != 0u || ptype == SPHERE || P.riseAll != 0u;
+    ps.bounce = ((ps.bounce & 0xffffu) + 1u) | (rise ? kRiseBit : 0u);
     return false;
 }
 
@@ -1205,10 +1206,9 @@ PT_DEV void finish_path(const TraceParams& P, PathState& ps, Xorwow& rng, float 
     }
     if (ps.alive) {
         camera_ray(P, fx, fy, rng, ps.o, ps.d);
-        ps.rise = P.camRise != 0u;
         ps.L = splat(0.0f);
         ps.T = splat(1.0f);
-        ps.bounce = 0;
+        ps.bounce = P.camRise ? kRiseBit : 0u;
     }
 }
 
@@ -1407,10 +1407,9 @@ PT_DEV void ssg_finish(const TraceParams& P, PathState& ps, Xorwow& rng, float f
         return;
     }
     camera_ray(P, fx, fy, rng, ps.o, ps.d);
-    ps.rise = P.camRise != 0u;
     ps.L = splat(0.0f);
     ps.T = splat(1.0f);
-    ps.bounce = 0;
+    ps.bounce = P.camRise ? kRiseBit : 0u;
 }
 
 struct PixelCtx {
@@ -1565,7 +1564,7 @@ __global__ void __launch_bounds__(WPB * 64, MINW) trace_kernel(TraceParams P)
         else load_pixel<AUX>(P, pc, rng, ps, accL);
         float fx = (float)(int32_t)pc.px, fy = (float)(int32_t)pc.py;
         camera_ray(P, fx, fy, rng, ps.o, ps.d);
-        ps.rise = P.camRise != 0u;
+        ps.bounce = P.camRise ? kRiseBit : 0u;
         uint32_t stripK = 0;                     // STRIP: this lane's tile within the unit
         uint64_t tAll = STATS ? __builtin_amdgcn_s_memtime() : 0;
         uint64_t tDone = 0;
@@ -1586,7 +1585,7 @@ __global__ void __launch_bounds__(WPB * 64, MINW) trace_kernel(TraceParams P)
                 bool tdone = true;
                 if (!held) {
                     tdone = traverse_cb_phase<STATS, WW % 100, QUAD>(nodes, prims, reinterpret_cast<uint2*>(stack), P,
-                                                                ps.o, ps.d, ps.rise, fresh, ts, cnt);
+                                                                ps.o, ps.d, (ps.bounce & kRiseBit) != 0u, fresh, ts, cnt);
                     fresh = tdone;
                 }
                 if (DEFERQ > 0 || SKYQ > 0) {
@@ -1620,7 +1619,7 @@ __global__ void __launch_bounds__(WPB * 64, MINW) trace_kernel(TraceParams P)
                             fx = (float)(int32_t)pc.px;
                             fy = (float)(int32_t)pc.py;
                             camera_ray(P, fx, fy, rng, ps.o, ps.d);
-                            ps.rise = P.camRise != 0u;
+                            ps.bounce = P.camRise ? kRiseBit : 0u;
                         }
                     }
                 }
@@ -1631,7 +1630,7 @@ __global__ void __launch_bounds__(WPB * 64, MINW) trace_kernel(TraceParams P)
         while (WW < 100 && ps.alive) {
             if (STATS) { cnt.segments++; wave_tick(cnt.w_segments); }
             float t;
-            const uint32_t e = WW >= 3 ? traverse_cb<STATS>(nodes, prims, reinterpret_cast<uint2*>(stack), P, ps.o, ps.d, ps.rise, t, cnt)
+            const uint32_t e = WW >= 3 ? traverse_cb<STATS>(nodes, prims, reinterpret_cast<uint2*>(stack), P, ps.o, ps.d, (ps.bounce & kRiseBit) != 0u, t, cnt)
                                        : traverse<STATS, WW>(nodes, prims, stack, ps.o, ps.d, P.slabFast != 0, t, cnt);
             uint64_t tS = STATS ? __builtin_amdgcn_s_memtime() : 0;
             if (shade<STATS>(P, prims, e, t, ps, rng, cnt)) {
@@ -2609,7 +2608,7 @@ PT_API int pt_set_scene(pt_context* ctx, const pt_bvh_node* nodes, uint32_t node
     }
     // Rising t_max (ChildPair): a ray can meet a sphere with t0 <= t_min only if its origin lies in
     // the sphere or within t_min of it.  Origins lie on primitives (and at the camera, render_impl),
-    // so primitive i is flagged (hp[4 i + 3].y bit 0) when its box meets the box of another sphere
+    // so primitive i is flagged (bit 0 of its material record's third word, read by shade) when its box meets the box of another sphere
     // grown by a margin (t_min + rounding of hit points).  Boxes: every shape lies in [-1, 1]^3 of its
     // object space (Hittable.inl), so the world box is center + |M| * (1, 1, 1) with M the inverse of
     // the 3x3 part of inv_transform_rows; computed in double and grown by a relative 1e-4.
@@ -2683,10 +2682,10 @@ PT_API int pt_set_scene(pt_context* ctx, const pt_bvh_node* nodes, uint32_t node
         hp[4 * i + 0] = make_float4(R[0][0], R[1][0], R[0][1], R[1][1]);
         hp[4 * i + 1] = make_float4(R[0][2], R[1][2], R[0][3], R[1][3]);
         hp[4 * i + 2] = make_float4(R[2][0], R[2][1], R[2][2], R[2][3]);
-        hp[4 * i + 3] = make_float4(u2f(h.type), u2f(riseFlag[i]), 0.0f, 0.0f);
+        hp[4 * i + 3] = make_float4(u2f(h.type), 0.0f, 0.0f, 0.0f);
         hm[3 * i] = make_float4(h.base_color[0], h.base_color[1], h.base_color[2], h.roughness);
         hm[3 * i + 1] = make_float4(h.emissive[0], h.emissive[1], h.emissive[2], h.metalness);
-        hm[3 * i + 2] = make_float4(u2f(h.texture_index), u2f(h.material_type), 0.0f, 0.0f);
+        hm[3 * i + 2] = make_float4(u2f(h.texture_index), u2f(h.material_type), u2f(riseFlag[i]), 0.0f);
     }
     PT_HIP_CHECK(ctx, hipSetDevice(ctx->device));
     PT_HIP_CHECK(ctx, hipStreamSynchronize(ctx->stream));
