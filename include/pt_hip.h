@@ -202,7 +202,7 @@ PT_API int pt_read_tile_costs(pt_context *ctx, uint32_t *dst, uint32_t count);
 PT_API int pt_read_tile_idle(pt_context *ctx, uint32_t *dst, uint32_t count);
 
 /* Tuning knob for A/B measurements: 0 = automatic (default); otherwise one of the shipped
- * trace-kernel variants 1, 4, 6, 20, 39, 40, 41, 46, 47, 48, 59, 60, 61, 66, 67 (traversal loop shape, deferred shading,
+ * trace-kernel variants 1, 4, 6, 20, 39, 40, 41, 46, 47, 48 (traversal loop shape, deferred shading,
  * BVH staged in LDS or read through the caches, occupancy target; see pt_kernels.hip).  All variants
  * produce bit-identical results.  Other numbers return PT_ERR_ARG. */
 PT_API int pt_set_kernel_variant(pt_context *ctx, int variant);
@@ -239,10 +239,10 @@ PT_API int pt_set_issue_priority(pt_context *ctx, int mode, uint32_t level3, uin
  * 0 = automatic (K = 4 at <= 2 samples per pixel on large images), 1 = off, K = 2..16 = always K
  * (resumable variants).  Results are identical for every setting. */
 PT_API int pt_set_strip_units(pt_context *ctx, int mode);
-/* Check mode for the rising-t_max rule (the sphere's far-root quirk can raise t_max mid-traversal,
- * pt_kernels.hip ChildPair): 1 = every ray keeps pending far children for a test at pop time (the
- * reference's rule, slower), 0 = only rays the host flags (origin possibly in or near a sphere).
- * Both give the reference's results; tests compare them. */
+/* Check mode for a rising t_max (the sphere's far-root quirk can raise t_max mid-traversal,
+ * pt_kernels.hip ChildPair): 1 = every ray keeps every far child it meets for a test at pop time
+ * (the reference's rule, slower); 0 (default) = far children are kept when hit now, and the pending
+ * set is rebuilt when a leaf raises t_max.  Both give the reference's results; tests compare them. */
 PT_API int pt_set_rise_check(pt_context *ctx, int all_rays);
 PT_API int pt_set_sample_groups(pt_context *ctx, int mode);
 PT_API int pt_set_patch_rounds(pt_context *ctx, uint32_t rounds);

@@ -76,8 +76,6 @@ struct TraceParams {
     uint32_t nodeCount, primCount, stackDepth, slabFast;
     const float4* cnodes;       // child-box records (4 per interior node), see traverse_cb
     uint32_t cnodeCount, rootWord;
-    const float4* qnodes;       // 4-wide child-box records (8 per even-depth interior node), see walk_interior_quad
-    uint32_t qnodeCount, qrootWord, qstackDepth;
     float rootBox[6];           // (min.x, max.x, min.y, max.y, min.z, max.z) of the root
     const uint32_t* order;      // tile dispatch order as packed tile coordinates (tileY << 16 | tileX),
                                 // see "Tile scheduling"; null only with scatterWaves
@@ -111,8 +109,8 @@ struct TraceParams {
     uint32_t occCap;            // host only: persistent grids hold at most this many workgroups per CU (0 = all)
     uint32_t prio[3];           // issue priority by order position: < prio[0] -> 3, < prio[1] -> 2, < prio[2] -> 1
     uint32_t strip;             // MODE 3: tiles per dispatch unit (a row strip of `strip` tiles; see trace_kernel)
-    uint32_t camRise;           // the camera lies in or near a sphere (primary rays: SlabRay::rise)
-    uint32_t riseAll;           // check mode (pt_set_rise_check): every ray keeps far children for a later test
+    uint32_t riseAll;           // every ray keeps far children for a test at pop time (ChildPair): the check
+                                // mode pt_set_rise_check, or a BVH whose leaves are not in DFS prim order
 };
 
 // Speculative sample groups: window of a group's start offset in which an earlier group's parse can
@@ -561,7 +559,6 @@ struct SlabRay {
     f3 o;
     float ix, iy, iz;
     bool fast;
-    bool rise;                  // t_max may rise on this ray (its origin may lie in or near a sphere, ChildPair)
 };
 
 // lo and X of one box (see above); the fast form under the same conditions as node_test_fast.
@@ -598,24 +595,19 @@ PT_DEV float slab_lo_x(const SlabRay& R, f2v bx, f2v by, f2v bz, float tMin, flo
 // selects pick the next node, the far node and its entry distance.
 // t_max can RISE during a traversal: the sphere's far-root quirk (Hittable.inl:158, prim_hit_rec)
 // accepts t1 > t_max when t0 <= t_min, and the reference then tests the boxes it pops with that
-// larger t_max.  A far child that fails its test now would pass it later, so on such a ray a pending
-// child may be dropped only for a reason that does not depend on t_max: the far child is pushed when
-// the near one is hit now and the far box meets the ray at all (X > lo), and whether it still passes
-// is decided when it is popped (t_max > lo), as in trace.cu:48-98.  t0 <= t_min needs the ray origin
-// inside a sphere or within t_min of it; rays whose origin cannot be (SlabRay::rise false, decided per
-// primitive and camera on the host, pt_set_scene / render_impl) keep a far child only if it is hit now.
+// larger t_max (trace.cu:48-98).  The walks keep a far child only if it is hit at the current t_max
+// (`push`) -- exact while t_max only falls -- and rebuild the pending set when a leaf raises it
+// (repair_pending).  RISEALL (wave-uniform: the check mode, or a BVH the rebuild cannot descend)
+// keeps a far child whenever its box meets the ray at all, the reference's own rule.
 struct ChildPair {
-    bool push, any;             // push: the near child is hit and the far box meets the ray; any: a child is hit
+    bool push, any;             // push: keep the far child for a test at pop time; any: a child is hit
     uint32_t wNext, wF;         // next node (the near one when both hit), far node
     float loNext, loF;          // their slab entry distances
-    bool gBoth, gAny;           // both / any child box meets the ray (t_max-free: the 4-wide far side)
-    uint32_t wG;                // the one child that meets the ray when only one does
-    float loG, loMin;           // its lo; the smaller lo of the two
 };
 
 template <bool ALLFAST = false>
 PT_DEV ChildPair cb_pair(const float4& Q0, const float4& Q1, const float4& Q2, const float4& Q3, const SlabRay& R,
-                         uint32_t negMask, float tMin, float tMax)
+                         uint32_t negMask, float tMin, float tMax, bool riseAll)
 {
     float XL, XR;
     const float loL = slab_lo_x<ALLFAST>(R, f2(Q0.x, Q0.y), f2(Q0.z, Q0.w), f2(Q1.x, Q1.y), tMin, XL);
@@ -624,29 +616,50 @@ PT_DEV ChildPair cb_pair(const float4& Q0, const float4& Q1, const float4& Q2, c
     const uint32_t wL = __float_as_uint(Q3.x), wR = __float_as_uint(Q3.y);
     const bool hL = XL > loL && tMax > loL;
     const bool hR = XR > loR && tMax > loR;
-    const bool gL = XL > loL && (R.rise || tMax > loL), gR = XR > loR && (R.rise || tMax > loR);   // kept for later
     const bool takeL = hL && (!hR || !isNeg);
     ChildPair c;
-    c.push = isNeg ? (hR && gL) : (hL && gR);
+    c.push = riseAll ? (isNeg ? (hR && XL > loL) : (hL && XR > loR)) : (hL && hR);
     c.any = hL || hR;
     c.wNext = takeL ? wL : wR;
     c.loNext = takeL ? loL : loR;
     c.wF = isNeg ? wL : wR;
     c.loF = isNeg ? loL : loR;
-    c.gBoth = gL && gR;
-    c.gAny = gL || gR;
-    c.wG = gL ? wL : wR;
-    c.loG = gL ? loL : loR;
-    c.loMin = __builtin_fminf(loL, loR);
     return c;
 }
 
 template <bool ALLFAST = false>
 PT_DEV ChildPair cb_children(const float4* __restrict__ cnodes, uint32_t cur, const SlabRay& R, uint32_t negMask,
-                             float tMin, float tMax)
+                             float tMin, float tMax, bool riseAll)
 {
     return cb_pair<ALLFAST>(cnodes[4 * cur], cnodes[4 * cur + 1], cnodes[4 * cur + 2], cnodes[4 * cur + 3], R, negMask,
-                            tMin, tMax);
+                            tMin, tMax, riseAll);
+}
+
+// The reference's pending far children at leaf `leafOff` (after a leaf raised t_max): its stack
+// holds, for every interior node on the path to the leaf where the path took the near child, the
+// far child (trace.cu:75) -- bottom to top in path order.  The path is found from the root by the
+// first primitive of each second child (child-box record Q3.w; leaves hold their primitives in DFS
+// order, host-checked), and a far child whose box the ray does not meet at all (X <= lo) is left out
+// (no t_max makes it pass).  Rebuilt entries include every one the walk kept, so the lane resumes
+// exactly where the reference stands.
+PT_DEV void repair_pending(const float4* __restrict__ cnodes, uint2* stack, const SlabRay& R, uint32_t negMask, float tMin,
+                           uint32_t rootWord, uint32_t leafOff, uint32_t& sp)
+{
+    sp = 0;
+    uint32_t n = rootWord;
+    while ((n >> 24) == 0u) {
+        const float4 Q0 = cnodes[4 * n], Q1 = cnodes[4 * n + 1], Q2 = cnodes[4 * n + 2], Q3 = cnodes[4 * n + 3];
+        const bool inR = leafOff >= __float_as_uint(Q3.w);
+        const bool isNeg = (negMask & __float_as_uint(Q3.z)) != 0u;   // near child = second when negative
+        float X;                                                     // the other child's box (Q0..Q2 layout)
+        const float lo = slab_lo_x(R, inR ? f2(Q0.x, Q0.y) : f2(Q2.x, Q2.y), inR ? f2(Q0.z, Q0.w) : f2(Q2.z, Q2.w),
+                                   inR ? f2(Q1.x, Q1.y) : f2(Q1.z, Q1.w), tMin, X);
+        if (inR == isNeg && X > lo) {                                // the path took the near child
+            stack[64u * sp] = make_uint2(__float_as_uint(inR ? Q3.x : Q3.y), __float_as_uint(lo));
+            ++sp;
+        }
+        n = __float_as_uint(inR ? Q3.y : Q3.x);
+    }
 }
 
 // The interior walk of the resumable traversal (trace.cu:66-77 per visited node): descend until a
@@ -658,11 +671,11 @@ PT_DEV ChildPair cb_children(const float4* __restrict__ cnodes, uint32_t cur, co
 // entries -- with the stack pointer advanced only when the far child is to be kept (ChildPair).
 template <bool STATS, bool ALLFAST>
 PT_DEV bool walk_interior(const float4* __restrict__ cnodes, uint2* stack, const SlabRay& R, uint32_t negMask,
-                          float tMin, float tMax, uint32_t& cur, uint32_t& sp, Counters& cnt)
+                          float tMin, float tMax, bool riseAll, uint32_t& cur, uint32_t& sp, Counters& cnt)
 {
     while ((cur >> 24) == 0u) {
         if (STATS) { cnt.node_tests += 2; wave_tick(cnt.w_node); }
-        const ChildPair ch = cb_children<ALLFAST>(cnodes, cur, R, negMask, tMin, tMax);
+        const ChildPair ch = cb_children<ALLFAST>(cnodes, cur, R, negMask, tMin, tMax, riseAll);
         stack[64u * sp] = make_uint2(ch.wF, __float_as_uint(ch.loF));
         sp += ch.push ? 1u : 0u;
         if (ch.any) {
@@ -679,93 +692,14 @@ PT_DEV bool walk_interior(const float4* __restrict__ cnodes, uint2* stack, const
     return false;
 }
 
-// ---------------------------------------------------------------------------------------------
-// 4-wide child-box traversal (QUAD).  Device layout "qnodes": one 128-byte record per interior node
-// at EVEN depth of the reference BVH (a "landing" node N; root = depth 0), two halves of the
-// child-box format above:
-//   half 0 = N's first child A = N + 1:  A interior -> A's two children (A + 1, A.offset) with their
-//            boxes and words and 1 << A's split axis; A a leaf -> slot L = A itself, slot R empty
-//   half 1 = N's second child B = N.offset, the same.
-// A child word is (count << 24 | prim offset) for a leaf, the record index of an even-depth
-// interior node with that node's split axis at bit 20 (axis << 20 | r, r < 2^20), or a PAIR
-// reference (1 << 23 | 2 r + h): "half h of record r" -- the odd-depth node whose two children that
-// half holds.  An empty slot has the box [+inf, +inf]^3, which no ray
-// hits in either slab form.
-//
-// A landing visit tests the four grandchild boxes (or the leaf children) at once, with one 128-byte
-// fetch, instead of visiting N and then its near child with two dependent fetches.  Exactness: the
-// slab test of a child box nested in its parent's (host-checked: min >= parent min, max <= parent
-// max, no NaN) can only pass if the parent's passes -- per axis the child's slab interval lies
-// inside the parent's, in float arithmetic too (subtraction and multiplication round
-// monotonically; an infinite 1/d gives both boxes the same +-inf or no-constraint NaN bound) -- so
-// testing the near child's children directly gives the reference's verdicts (trace.cu:48-77: near
-// child tested at the same t_max, then its children at the same t_max).  The far side is pushed as
-// ONE entry, as the reference pushes the far child (trace.cu:75), decided without t_max (which can
-// rise before the pop, ChildPair): if both of its child boxes meet the ray, a PAIR reference with
-// lo = the smaller of their entry distances -- popped with t_max <= lo neither child can pass,
-// otherwise the pair is visited and both children are tested with the then-current t_max, exactly
-// the reference's visit of the far child (its own box test implied by nesting); if one does, that
-// child's word and lo, as a plain far entry; if none, nothing (no t_max can make it pass).  A pair
-// visit fetches the same record and enables only its half.  Visit order, node culling and primitive tests per lane are the
-// reference's; the stack holds at most the reference's pending count (<= one entry per level).
-// ---------------------------------------------------------------------------------------------
-constexpr uint32_t kPairBit = 1u << 23;
-constexpr uint32_t kQuadAxisShift = 20;                  // landing word: record | N's split axis << 20
-constexpr uint32_t kQuadRecMask = (1u << kQuadAxisShift) - 1u;
-constexpr uint32_t kQuadPairMask = (1u << (kQuadAxisShift + 1)) - 1u;   // pair word: 2 r + h
-
-template <bool STATS, bool ALLFAST>
-PT_DEV bool walk_interior_quad(const float4* __restrict__ qnodes, uint2* stack, const SlabRay& R, uint32_t negMask,
-                               float tMin, float tMax, uint32_t& cur, uint32_t& sp, Counters& cnt)
-{
-    while ((cur >> 24) == 0u) {
-        if (STATS) { cnt.node_tests += 2; wave_tick(cnt.w_node); }   // one visit (bench.lane_utilisation)
-        const bool isPair = (cur & kPairBit) != 0u;
-        const uint32_t r = isPair ? (cur & (kQuadPairMask)) >> 1 : cur & kQuadRecMask;
-        // near side: by N's split axis (carried in the landing word, trace.cu:69-76), the referenced
-        // half on a pair visit -- known before the record arrives, so the halves load in visit order
-        const uint32_t nearIsB = isPair ? (cur & 1u) : (negMask >> ((cur >> kQuadAxisShift) & 3u)) & 1u;
-        const float4* qn = qnodes + 8 * r + 4 * nearIsB;
-        const float4* qf = qnodes + 8 * r + 4 * (nearIsB ^ 1u);
-        const ChildPair nr = cb_pair<ALLFAST>(qn[0], qn[1], qn[2], qn[3], R, negMask, tMin, tMax);
-        const ChildPair fr = cb_pair<ALLFAST>(qf[0], qf[1], qf[2], qf[3], R, negMask, tMin, tMax);
-        // descend into the near side if any of its children passes, else into the far side (same t_max)
-        const bool intoNear = nr.any;
-        const bool farOn = !isPair && fr.any;
-        const ChildPair& sd = intoNear ? nr : fr;
-        // entry 1: the far side, below the near side's far child, kept when descending near and any of
-        // its child boxes meets the ray (t_max-free, see ChildPair): a pair reference when both do
-        const uint32_t w1 = fr.gBoth ? (kPairBit | (2u * r + (nearIsB ^ 1u))) : fr.wG;
-        const float lo1 = fr.gBoth ? fr.loMin : fr.loG;
-        stack[64u * sp] = make_uint2(w1, __float_as_uint(lo1));
-        sp += (intoNear && !isPair && fr.gAny) ? 1u : 0u;
-        // entry 2: the far child of the side descended into (none when nothing is descended into:
-        // on a pair visit whose half misses, `fr` is the disabled half and must push nothing)
-        const bool descend = intoNear || farOn;
-        stack[64u * sp] = make_uint2(sd.wF, __float_as_uint(sd.loF));
-        sp += (descend && sd.push) ? 1u : 0u;
-        if (descend) {
-            cur = sd.wNext;
-        } else {
-            bool found = false;
-            while (sp > 0) {
-                const uint2 e = stack[64u * (--sp)];
-                if (tMax > __uint_as_float(e.y)) { cur = e.x; found = true; break; }
-            }
-            if (!found) return true;
-        }
-    }
-    return false;
-}
-
 template <bool STATS>
 PT_DEV uint32_t traverse_cb(const float4* __restrict__ cnodes, const float4* __restrict__ prims, uint2* stack,
-                            const TraceParams& P, f3 o, f3 d, bool rise, float& tHit, Counters& cnt)
+                            const TraceParams& P, f3 o, f3 d, float& tHit, Counters& cnt)
 {
     const float tMin = 0.001f;
     float tMax = kFltMax;
+    const bool riseAll = P.riseAll != 0u;
     SlabRay R;
-    R.rise = rise;
     R.o = o;
     R.ix = rcp_rn(d.x);
     R.iy = rcp_rn(d.y);
@@ -796,7 +730,7 @@ PT_DEV uint32_t traverse_cb(const float4* __restrict__ cnodes, const float4* __r
     while (!done) {
         while ((cur >> 24) == 0u) {                               // interior walk
             if (STATS) { cnt.node_tests += 2; wave_tick(cnt.w_node); }
-            const ChildPair ch = cb_children(cnodes, cur, R, negMask, tMin, tMax);   // trace.cu:66-77
+            const ChildPair ch = cb_children(cnodes, cur, R, negMask, tMin, tMax, riseAll);   // trace.cu:66-77
             if (ch.push) {
                 stack[64u * sp] = make_uint2(ch.wF, __float_as_uint(ch.loF));
                 ++sp;
@@ -811,17 +745,21 @@ PT_DEV uint32_t traverse_cb(const float4* __restrict__ cnodes, const float4* __r
         if (STATS) wave_time(cnt.cyc_node, tPhase);
         if (done) break;
         uint32_t leafOff = cur & 0xffffffu, leafCnt = cur >> 24;  // in-order leaf tests
+        const uint32_t leaf0 = leafOff;
+        bool rose = false;
         if (STATS) leaf_round_stats(prims, leafOff, leafCnt, cnt);
         while (leafCnt > 0) {
             if (STATS) { cnt.prim_tests++; wave_tick(cnt.w_prim); leaf_position_stats(prims, leafOff, cnt); }
             float t;
             if (prim_hit(prims, leafOff, o, d, tMin, tMax, t)) {
+                rose = rose || t > tMax;                          // the sphere's far-root quirk (ChildPair)
                 tMax = t;
                 elem = leafOff;
             }
             ++leafOff;
             --leafCnt;
         }
+        if (rose && !riseAll) repair_pending(cnodes, stack, R, negMask, tMin, P.rootWord, leaf0, sp);
         if (STATS) wave_time(cnt.cyc_leaf, tPhase);
         if (!pop()) done = true;
     }
@@ -844,13 +782,13 @@ struct TravState {
 
 // The interior walk is walk_interior (the lean form: wave-uniform slab-form choice, unconditional
 // far-child write).  WW = 200 + EXITQ selects this traversal.
-template <bool STATS, int EXITQ, bool QUAD = false>
+template <bool STATS, int EXITQ>
 PT_DEV bool traverse_cb_phase(const float4* __restrict__ cnodes, const float4* __restrict__ prims, uint2* stack,
-                              const TraceParams& P, f3 o, f3 d, bool rise, bool fresh, TravState& ts, Counters& cnt)
+                              const TraceParams& P, f3 o, f3 d, bool fresh, TravState& ts, Counters& cnt)
 {
     const float tMin = 0.001f;
+    const bool riseAll = P.riseAll != 0u;
     SlabRay R;
-    R.rise = rise;
     R.o = o;
     R.ix = rcp_rn(d.x);
     R.iy = rcp_rn(d.y);
@@ -869,7 +807,7 @@ PT_DEV bool traverse_cb_phase(const float4* __restrict__ cnodes, const float4* _
         ts.tMax = kFltMax;
         ts.sp = 0;
         ts.elem = 0xffffffffu;
-        ts.cur = QUAD ? P.qrootWord : P.rootWord;
+        ts.cur = P.rootWord;
         if (STATS) { cnt.node_tests++; wave_tick(cnt.w_node); }
         float X;
         const float lo0 = slab_lo_x(R, f2(P.rootBox[0], P.rootBox[1]), f2(P.rootBox[2], P.rootBox[3]),
@@ -888,26 +826,26 @@ PT_DEV bool traverse_cb_phase(const float4* __restrict__ cnodes, const float4* _
     uint64_t tPhase = STATS ? __builtin_amdgcn_s_memtime() : 0;
     const bool allFast = __ballot(!R.fast) == 0;                         // wave-uniform
     while (!done) {
-        if (QUAD)
-            done = allFast ? walk_interior_quad<STATS, true>(cnodes, stack, R, negMask, tMin, tMax, cur, sp, cnt)
-                           : walk_interior_quad<STATS, false>(cnodes, stack, R, negMask, tMin, tMax, cur, sp, cnt);
-        else
-            done = allFast ? walk_interior<STATS, true>(cnodes, stack, R, negMask, tMin, tMax, cur, sp, cnt)
-                           : walk_interior<STATS, false>(cnodes, stack, R, negMask, tMin, tMax, cur, sp, cnt);
+        done = allFast ? walk_interior<STATS, true>(cnodes, stack, R, negMask, tMin, tMax, riseAll, cur, sp, cnt)
+                       : walk_interior<STATS, false>(cnodes, stack, R, negMask, tMin, tMax, riseAll, cur, sp, cnt);
         if (STATS) wave_time(cnt.cyc_node, tPhase);
         if (done) break;
         uint32_t leafOff = cur & 0xffffffu, leafCnt = cur >> 24;
+        const uint32_t leaf0 = leafOff;
+        bool rose = false;
         if (STATS) leaf_round_stats(prims, leafOff, leafCnt, cnt);
         while (leafCnt > 0) {
             if (STATS) { cnt.prim_tests++; wave_tick(cnt.w_prim); leaf_position_stats(prims, leafOff, cnt); }
             float t;
             if (prim_hit(prims, leafOff, o, d, tMin, tMax, t)) {
+                rose = rose || t > tMax;                          // the sphere's far-root quirk (ChildPair)
                 tMax = t;
                 elem = leafOff;
             }
             ++leafOff;
             --leafCnt;
         }
+        if (rose && !riseAll) repair_pending(cnodes, stack, R, negMask, tMin, P.rootWord, leaf0, sp);
         if (STATS) wave_time(cnt.cyc_leaf, tPhase);
         if (!pop()) { done = true; break; }
         // early exit once at most EXITQ/64 of the lanes that entered are still walking
@@ -1049,12 +987,9 @@ struct PathState {
     f3 color;         // sum of the finished paths of the current render() call (trace.cu:186)
     uint32_t acc;     // float index of this lane's running accumulation value in the dynamic LDS
                       // (x, y, z at lds_f()[acc], [acc + 64], [acc + 128])
-    uint32_t s, c;
-    uint32_t bounce;  // segments of this path so far (bits 0-15) | kRiseBit: the current ray's origin
-                      // may lie in or near a sphere (ChildPair, host flags), kept in the same register
+    uint32_t s, c, bounce;
     bool alive;
 };
-constexpr uint32_t kRiseBit = 1u << 16;
 
 // camera ray of one sample (trace.cu:190-192, Camera.inl:25-28): two uniforms, x then y
 PT_DEV void camera_ray(const TraceParams& P, float fx, float fy, Xorwow& rng, f3& o, f3& d)
@@ -1095,7 +1030,7 @@ PT_DEV bool shade(const TraceParams& P, const float4* __restrict__ prims, uint32
     const float4 q2 = prims[4 * e + 2];
     const uint32_t ptype = __float_as_uint(prims[4 * e + 3].x);
     ps.L = add(ps.L, mul(ps.T, mk(m1.x, m1.y, m1.z)));                      // trace.cu:139
-    if ((ps.bounce & 0xffffu) == 4) {
+    if (ps.bounce == 4) {
         // 5th segment: its scattered ray is discarded (trace.cu:109); only the two uniforms of
         // Material.inl:40-41 are observable.
         (void)uniform(rng);
@@ -1174,11 +1109,7 @@ PT_DEV bool shade(const TraceParams& P, const float4* __restrict__ prims, uint32
     ps.T = mul(ps.T, w);
     ps.o = sf.p;
     ps.d = sd;
-    // the new ray starts on primitive e: it may start in or near a sphere if e's box meets another
-    // sphere's (host flag), or if e is a sphere -- its rounded hit point may lie inside it, and a
-    // grazing ray from there meets its far side beyond t_min on a large sphere
-    const bool rise = (__float_as_uint(m2.z) & 1u) != 0u || ptype == SPHERE || P.riseAll != 0u;
-    ps.bounce = ((ps.bounce & 0xffffu) + 1u) | (rise ? kRiseBit : 0u);
+    ++ps.bounce;
     return false;
 }
 
@@ -1208,7 +1139,7 @@ PT_DEV void finish_path(const TraceParams& P, PathState& ps, Xorwow& rng, float 
         camera_ray(P, fx, fy, rng, ps.o, ps.d);
         ps.L = splat(0.0f);
         ps.T = splat(1.0f);
-        ps.bounce = P.camRise ? kRiseBit : 0u;
+        ps.bounce = 0;
     }
 }
 
@@ -1409,7 +1340,7 @@ PT_DEV void ssg_finish(const TraceParams& P, PathState& ps, Xorwow& rng, float f
     camera_ray(P, fx, fy, rng, ps.o, ps.d);
     ps.L = splat(0.0f);
     ps.T = splat(1.0f);
-    ps.bounce = P.camRise ? kRiseBit : 0u;
+    ps.bounce = 0;
 }
 
 struct PixelCtx {
@@ -1512,12 +1443,9 @@ __global__ void __launch_bounds__(WPB * 64, MINW) trace_kernel(TraceParams P)
     constexpr bool SSG = MODE == 1, AUX = MODE == 2, STRIP = MODE == 3;
     const uint32_t lane = threadIdx.x & 63u;
     const uint32_t wave = threadIdx.x >> 6;
-    // QUAD (WW / 100000 == 1): the 4-wide child-box walk over qnodes (walk_interior_quad), with its
-    // own stack bound (pt_set_scene)
-    constexpr bool QUAD = WW >= 100 && (WW / 100000) % 10 == 1;
-    const float4* gnodes = QUAD ? P.qnodes : (WW >= 3 ? P.cnodes : P.nodes);
-    const uint32_t nodeF4 = QUAD ? 8u * P.qnodeCount : (WW >= 3 ? 4u * P.cnodeCount : 2u * P.nodeCount);
-    const uint32_t stackDepth = QUAD ? P.qstackDepth : P.stackDepth;
+    const float4* gnodes = WW >= 3 ? P.cnodes : P.nodes;
+    const uint32_t nodeF4 = WW >= 3 ? 4u * P.cnodeCount : 2u * P.nodeCount;
+    const uint32_t stackDepth = P.stackDepth;
     const uint32_t sceneF4 = (SL >= 1 ? nodeF4 : 0u) + (SL >= 2 ? 4u * P.primCount : 0u);
     if (SL >= 1) {
         for (uint32_t i = threadIdx.x; i < nodeF4; i += WPB * 64) lds4[i] = gnodes[i];
@@ -1564,7 +1492,6 @@ __global__ void __launch_bounds__(WPB * 64, MINW) trace_kernel(TraceParams P)
         else load_pixel<AUX>(P, pc, rng, ps, accL);
         float fx = (float)(int32_t)pc.px, fy = (float)(int32_t)pc.py;
         camera_ray(P, fx, fy, rng, ps.o, ps.d);
-        ps.bounce = P.camRise ? kRiseBit : 0u;
         uint32_t stripK = 0;                     // STRIP: this lane's tile within the unit
         uint64_t tAll = STATS ? __builtin_amdgcn_s_memtime() : 0;
         uint64_t tDone = 0;
@@ -1584,8 +1511,8 @@ __global__ void __launch_bounds__(WPB * 64, MINW) trace_kernel(TraceParams P)
                 if (STATS && fresh && !held) { cnt.segments++; wave_tick(cnt.w_segments); }
                 bool tdone = true;
                 if (!held) {
-                    tdone = traverse_cb_phase<STATS, WW % 100, QUAD>(nodes, prims, reinterpret_cast<uint2*>(stack), P,
-                                                                ps.o, ps.d, (ps.bounce & kRiseBit) != 0u, fresh, ts, cnt);
+                    tdone = traverse_cb_phase<STATS, WW % 100>(nodes, prims, reinterpret_cast<uint2*>(stack), P,
+                                                                ps.o, ps.d, fresh, ts, cnt);
                     fresh = tdone;
                 }
                 if (DEFERQ > 0 || SKYQ > 0) {
@@ -1619,7 +1546,6 @@ __global__ void __launch_bounds__(WPB * 64, MINW) trace_kernel(TraceParams P)
                             fx = (float)(int32_t)pc.px;
                             fy = (float)(int32_t)pc.py;
                             camera_ray(P, fx, fy, rng, ps.o, ps.d);
-                            ps.bounce = P.camRise ? kRiseBit : 0u;
                         }
                     }
                 }
@@ -1630,7 +1556,7 @@ __global__ void __launch_bounds__(WPB * 64, MINW) trace_kernel(TraceParams P)
         while (WW < 100 && ps.alive) {
             if (STATS) { cnt.segments++; wave_tick(cnt.w_segments); }
             float t;
-            const uint32_t e = WW >= 3 ? traverse_cb<STATS>(nodes, prims, reinterpret_cast<uint2*>(stack), P, ps.o, ps.d, (ps.bounce & kRiseBit) != 0u, t, cnt)
+            const uint32_t e = WW >= 3 ? traverse_cb<STATS>(nodes, prims, reinterpret_cast<uint2*>(stack), P, ps.o, ps.d, t, cnt)
                                        : traverse<STATS, WW>(nodes, prims, stack, ps.o, ps.d, P.slabFast != 0, t, cnt);
             uint64_t tS = STATS ? __builtin_amdgcn_s_memtime() : 0;
             if (shade<STATS>(P, prims, e, t, ps, rng, cnt)) {
@@ -2062,10 +1988,8 @@ struct pt_context {
     float4* mats = nullptr;
     float4* cnodes = nullptr;   // child-box records (traverse_cb); null when the scene exceeds its encoding
     uint32_t cnodeCount = 0, rootWord = 0;
-    std::vector<double> sphereBoxes;  // per sphere: world box grown by the rising-t_max margin (pt_set_scene)
     bool riseAll = false;             // pt_set_rise_check
-    float4* qnodes = nullptr;   // 4-wide child-box records (walk_interior_quad); null when boxes are not nested
-    uint32_t qnodeCount = 0, qrootWord = 0, qstackDepth = 1;
+    bool dfsOrder = true;             // leaves hold their primitives in DFS order (repair_pending)
     float rootBox[6] = {};
     uint32_t nodeCount = 0, primCount = 0, stackDepth = 1;
     bool slabFast = true;
@@ -2154,12 +2078,9 @@ static int fail(pt_context* ctx, int code, const char* msg)
 template <bool STATS, int SL, int WPB, int WW, int MINW, bool PERSIST = false, int MODE = 0>
 static hipError_t launch_one(const TraceParams& P, hipStream_t stream)
 {
-    constexpr bool QUAD = WW >= 100 && (WW / 100000) % 10 == 1;
-    if (QUAD && P.qnodes == nullptr)           // no 4-wide layout (unnested boxes): the 2-wide walk
-        return launch_one<STATS, SL, WPB, WW % 100000, MINW, PERSIST, MODE>(P, stream);
-    const size_t nodeF4 = QUAD ? 8 * (size_t)P.qnodeCount : (WW >= 3 ? 4 * (size_t)P.cnodeCount : 2 * (size_t)P.nodeCount);
+    const size_t nodeF4 = WW >= 3 ? 4 * (size_t)P.cnodeCount : 2 * (size_t)P.nodeCount;
     const size_t sceneBytes = ((SL >= 1 ? nodeF4 : 0) + (SL >= 2 ? 4 * (size_t)P.primCount : 0)) * sizeof(float4);
-    const size_t lds = sceneBytes + (size_t)WPB * (QUAD ? P.qstackDepth : P.stackDepth) * 64 * (WW >= 3 ? 8 : 4) + (size_t)WPB * 64 * 12;
+    const size_t lds = sceneBytes + (size_t)WPB * P.stackDepth * 64 * (WW >= 3 ? 8 : 4) + (size_t)WPB * 64 * 12;
     if (WW >= 3 && P.cnodes == nullptr) return MODE == 1 ? hipErrorInvalidValue : launch_one<STATS, SL, WPB, 1, MINW, PERSIST, MODE>(P, stream);  // no child-box layout
     if (lds > 160 * 1024) {
         // scene too large to stage in LDS: the same variant reading the scene through the caches
@@ -2245,11 +2166,6 @@ static hipError_t launch_variant(int v, const TraceParams& P, hipStream_t stream
     case 46: return launch_one<STATS, 0, 4, 14212, 4, true, MODE>(P, stream);
     case 47: return launch_one<STATS, 1, 4, 224, 4, true, MODE>(P, stream);
     case 48: return launch_one<STATS, 2, 4, 13216, 4, true, MODE>(P, stream);
-    case 59: return launch_one<STATS, 1, 4, 100000 + 224, 5, true, MODE>(P, stream);
-    case 60: return launch_one<STATS, 1, 4, 100000 + kV40Walk, 5, true, MODE>(P, stream);
-    case 61: return launch_one<STATS, 0, 4, 100000 + 14212, 5, true, MODE>(P, stream);
-    case 66: return launch_one<STATS, 0, 4, 100000 + 14212, 4, true, MODE>(P, stream);
-    case 67: return launch_one<STATS, 1, 4, 100000 + 224, 4, true, MODE>(P, stream);
     default: return hipErrorInvalidValue;
     }
 }
@@ -2264,10 +2180,6 @@ static hipError_t launch_grouped(int v, const TraceParams& P, hipStream_t stream
     case 40: return launch_one<false, 1, 4, kV40Walk, 5, true, MODE>(P, stream);
     case 41: return launch_one<false, 0, 4, 14212, 5, true, MODE>(P, stream);
     case 46: return launch_one<false, 0, 4, 14212, 4, true, MODE>(P, stream);
-    case 59: return launch_one<false, 1, 4, 100000 + 224, 5, true, MODE>(P, stream);
-    case 60: return launch_one<false, 1, 4, 100000 + kV40Walk, 5, true, MODE>(P, stream);
-    case 61: return launch_one<false, 0, 4, 100000 + 14212, 5, true, MODE>(P, stream);
-    case 66: return launch_one<false, 0, 4, 100000 + 14212, 4, true, MODE>(P, stream);
     default: return hipErrorInvalidValue;
     }
 }
@@ -2279,14 +2191,11 @@ static hipError_t launch_strip(int v, const TraceParams& P, hipStream_t stream)
     case 40: return launch_one<false, 1, 4, kV40Walk, 5, true, 3>(P, stream);
     case 41: return launch_one<false, 0, 4, 14212, 5, true, 3>(P, stream);
     case 46: return launch_one<false, 0, 4, 14212, 4, true, 3>(P, stream);
-    case 60: return launch_one<false, 1, 4, 100000 + kV40Walk, 5, true, 3>(P, stream);
-    case 61: return launch_one<false, 0, 4, 100000 + 14212, 5, true, 3>(P, stream);
-    case 66: return launch_one<false, 0, 4, 100000 + 14212, 4, true, 3>(P, stream);
     default: return hipErrorInvalidValue;
     }
 }
 
-static bool strip_capable(int v) { return v == 40 || v == 41 || v == 46 || v == 60 || v == 61 || v == 66; }
+static bool strip_capable(int v) { return v == 40 || v == 41 || v == 46; }
 
 // Tiles per dispatch unit.  A launch of few samples per pixel idles the lanes whose pixels finish
 // first for the rest of their tile; strips of K tiles let those lanes go on with the next tile.
@@ -2312,8 +2221,7 @@ static uint32_t strip_tiles(const pt_context* ctx, int variant, uint32_t tiles, 
 
 static bool variant_shipped(int v)
 {
-    return v == 0 || v == 1 || v == 4 || v == 6 || v == 20 || v == 40 || v == 41 || v == 46 || v == 47 || v == 48 || v == 39 ||
-           v == 59 || v == 60 || v == 61 || v == 66 || v == 67;
+    return v == 0 || v == 1 || v == 4 || v == 6 || v == 20 || v == 40 || v == 41 || v == 46 || v == 47 || v == 48 || v == 39;
 }
 
 // Cost pre-pass of a cold-start launch (render_impl): samples per pixel, and the smallest launch
@@ -2449,7 +2357,6 @@ PT_API void pt_destroy(pt_context* ctx)
     (void)hipFree(ctx->prims);
     (void)hipFree(ctx->mats);
     (void)hipFree(ctx->cnodes);
-    (void)hipFree(ctx->qnodes);
     (void)hipFree(ctx->tileCost);
     (void)hipFree(ctx->tileIdle);
     (void)hipFree(ctx->order);
@@ -2547,6 +2454,23 @@ PT_API int pt_set_scene(pt_context* ctx, const pt_bvh_node* nodes, uint32_t node
         const uint32_t count = nodes[i].primitive_count_axis >> 16;
         return count ? (count << 24) | nodes[i].offset : rec[i];
     };
+    // first and last primitive under each node (children follow their parent in the array); the
+    // rising-t_max rebuild (repair_pending) finds a leaf's path by the first primitive of each
+    // second child, which needs every left subtree's primitives below the right subtree's
+    std::vector<uint32_t> firstPrim(node_count), lastPrim(node_count);
+    bool dfsOrder = true;
+    for (uint32_t i = node_count; i-- > 0;) {
+        const uint32_t count = nodes[i].primitive_count_axis >> 16;
+        if (count) {
+            firstPrim[i] = nodes[i].offset;
+            lastPrim[i] = nodes[i].offset + count - 1;
+        } else {
+            const uint32_t a = i + 1, b = nodes[i].offset;
+            firstPrim[i] = std::min(firstPrim[a], firstPrim[b]);
+            lastPrim[i] = std::max(lastPrim[a], lastPrim[b]);
+            if (!(lastPrim[a] < firstPrim[b])) dfsOrder = false;
+        }
+    }
     std::vector<float4> hc(4 * (size_t)std::max(interior, 1u), make_float4(0.0f, 0.0f, 0.0f, 0.0f));
     for (uint32_t i = 0; cbOk && i < node_count; ++i) {
         if (rec[i] == 0xffffffffu) continue;
@@ -2556,125 +2480,8 @@ PT_API int pt_set_scene(pt_context* ctx, const pt_bvh_node* nodes, uint32_t node
         q[0] = make_float4(L.aabb_min[0], L.aabb_max[0], L.aabb_min[1], L.aabb_max[1]);
         q[1] = make_float4(L.aabb_min[2], L.aabb_max[2], R.aabb_min[2], R.aabb_max[2]);
         q[2] = make_float4(R.aabb_min[0], R.aabb_max[0], R.aabb_min[1], R.aabb_max[1]);
-        q[3] = make_float4(u2f(word(i + 1)), u2f(word(nodes[i].offset)), u2f(1u << ((nodes[i].primitive_count_axis >> 8) & 0xffu)), 0.0f);
-    }
-    // 4-wide records (walk_interior_quad): interior nodes at even depth, in node order; every child
-    // box must lie inside its parent's (the exactness argument), else the 2-wide walk is used
-    std::vector<uint32_t> qrec(node_count, 0xffffffffu);
-    uint32_t quads = 0;
-    bool qOk = cbOk;
-    {
-        std::vector<uint8_t> depthOdd(node_count, 0);
-        for (uint32_t i = 0; qOk && i < node_count; ++i) {
-            if ((nodes[i].primitive_count_axis >> 16) != 0) continue;
-            for (const uint32_t c : {i + 1, nodes[i].offset}) {
-                depthOdd[c] = depthOdd[i] ^ 1u;            // parents precede children (validate_scene)
-                for (int k = 0; k < 3; ++k)
-                    if (!(nodes[c].aabb_min[k] >= nodes[i].aabb_min[k] && nodes[c].aabb_max[k] <= nodes[i].aabb_max[k]))
-                        qOk = false;
-            }
-            if (!depthOdd[i]) qrec[i] = quads++;
-        }
-        qOk = qOk && quads <= kQuadRecMask;
-    }
-    auto qword = [&](uint32_t i) {
-        const uint32_t count = nodes[i].primitive_count_axis >> 16;
-        return count ? (count << 24) | nodes[i].offset
-                     : qrec[i] | (((nodes[i].primitive_count_axis >> 8) & 0xffu) << kQuadAxisShift);
-    };
-    const float kInf = __builtin_inff();
-    std::vector<float4> hq(qOk ? 8 * (size_t)std::max(quads, 1u) : 0, make_float4(kInf, kInf, kInf, kInf));
-    for (uint32_t i = 0; qOk && i < node_count; ++i) {
-        if (qrec[i] == 0xffffffffu) continue;
-        float4* q = &hq[8 * (size_t)qrec[i]];
-        const uint32_t side[2] = {i + 1, nodes[i].offset};
-        for (int h = 0; h < 2; ++h, q += 4) {
-            const uint32_t c = side[h];
-            const bool leaf = (nodes[c].primitive_count_axis >> 16) != 0;
-            const pt_bvh_node& L = leaf ? nodes[c] : nodes[c + 1];
-            q[0] = make_float4(L.aabb_min[0], L.aabb_max[0], L.aabb_min[1], L.aabb_max[1]);
-            q[1] = make_float4(L.aabb_min[2], L.aabb_max[2], kInf, kInf);       // slot R empty for a leaf side
-            uint32_t wR = 0xffffffffu, axisBit = 0;
-            if (!leaf) {
-                const pt_bvh_node& R = nodes[nodes[c].offset];
-                q[1].z = R.aabb_min[2];
-                q[1].w = R.aabb_max[2];
-                q[2] = make_float4(R.aabb_min[0], R.aabb_max[0], R.aabb_min[1], R.aabb_max[1]);
-                wR = qword(nodes[c].offset);
-                axisBit = 1u << ((nodes[c].primitive_count_axis >> 8) & 0xffu);
-            }
-            q[3] = make_float4(u2f(leaf ? qword(c) : qword(c + 1)), u2f(wR), u2f(axisBit), 0.0f);
-        }
-    }
-    // Rising t_max (ChildPair): a ray can meet a sphere with t0 <= t_min only if its origin lies in
-    // the sphere or within t_min of it.  Origins lie on primitives (and at the camera, render_impl),
-    // so primitive i is flagged (bit 0 of its material record's third word, read by shade) when its box meets the box of another sphere
-    // grown by a margin (t_min + rounding of hit points).  Boxes: every shape lies in [-1, 1]^3 of its
-    // object space (Hittable.inl), so the world box is center + |M| * (1, 1, 1) with M the inverse of
-    // the 3x3 part of inv_transform_rows; computed in double and grown by a relative 1e-4.
-    std::vector<double> box(6 * (size_t)prim_count);
-    std::vector<uint32_t> spheres;
-    for (uint32_t i = 0; i < prim_count; ++i) {
-        const float(&A)[3][4] = prims[i].inv_transform_rows;
-        double a[3][3], m[3][3];
-        for (int r = 0; r < 3; ++r)
-            for (int c = 0; c < 3; ++c) a[r][c] = A[r][c];
-        const double det = a[0][0] * (a[1][1] * a[2][2] - a[1][2] * a[2][1]) - a[0][1] * (a[1][0] * a[2][2] - a[1][2] * a[2][0]) +
-                           a[0][2] * (a[1][0] * a[2][1] - a[1][1] * a[2][0]);
-        double* b = &box[6 * (size_t)i];
-        if (!(std::fabs(det) > 0.0) || !std::isfinite(det)) {   // degenerate: unbounded, flag everything
-            for (int k = 0; k < 3; ++k) { b[k] = -HUGE_VAL; b[3 + k] = HUGE_VAL; }
-        } else {
-            for (int r = 0; r < 3; ++r)
-                for (int c = 0; c < 3; ++c)
-                    m[r][c] = (a[(c + 1) % 3][(r + 1) % 3] * a[(c + 2) % 3][(r + 2) % 3] -
-                               a[(c + 1) % 3][(r + 2) % 3] * a[(c + 2) % 3][(r + 1) % 3]) / det;
-            for (int k = 0; k < 3; ++k) {
-                const double ctr = -(m[k][0] * A[0][3] + m[k][1] * A[1][3] + m[k][2] * A[2][3]);
-                const double ext = std::fabs(m[k][0]) + std::fabs(m[k][1]) + std::fabs(m[k][2]);
-                const double pad = 1e-4 * (std::fabs(ctr) + ext) + 1e-6;
-                b[k] = ctr - ext - pad;
-                b[3 + k] = ctr + ext + pad;
-            }
-        }
-        if (prims[i].type == SPHERE) spheres.push_back(i);
-    }
-    std::vector<uint32_t> riseFlag(prim_count, 0u);
-    ctx->sphereBoxes.clear();
-    {
-        const double margin = 0.01;             // > t_min (0.001) with room for rounding
-        for (const uint32_t si : spheres) {
-            const double* sb = &box[6 * (size_t)si];
-            for (int k = 0; k < 6; ++k) ctx->sphereBoxes.push_back(sb[k] + (k < 3 ? -margin : margin));
-        }
-        // per sphere, the primitives whose boxes meet its grown box, found through the BVH (its node
-        // boxes bound the primitives' geometry)
-        std::vector<uint32_t> st;
-        for (size_t j = 0; j < spheres.size(); ++j) {
-            const double* sb = &ctx->sphereBoxes[6 * j];
-            st.assign(1, 0u);
-            while (!st.empty()) {
-                const uint32_t n = st.back();
-                st.pop_back();
-                const pt_bvh_node& nd = nodes[n];
-                bool meet = true;
-                for (int k = 0; k < 3; ++k) meet = meet && nd.aabb_min[k] <= sb[3 + k] && nd.aabb_max[k] >= sb[k];
-                if (!meet) continue;
-                const uint32_t count = nd.primitive_count_axis >> 16;
-                if (count == 0) {
-                    st.push_back(n + 1);
-                    st.push_back(nd.offset);
-                    continue;
-                }
-                for (uint32_t i = nd.offset; i < nd.offset + count; ++i) {
-                    if (i == spheres[j] || riseFlag[i]) continue;
-                    const double* b = &box[6 * (size_t)i];
-                    bool m2 = true;
-                    for (int k = 0; k < 3; ++k) m2 = m2 && b[k] <= sb[3 + k] && b[3 + k] >= sb[k];
-                    if (m2) riseFlag[i] = 1u;
-                }
-            }
-        }
+        q[3] = make_float4(u2f(word(i + 1)), u2f(word(nodes[i].offset)), u2f(1u << ((nodes[i].primitive_count_axis >> 8) & 0xffu)),
+                           u2f(firstPrim[nodes[i].offset]));
     }
     for (uint32_t i = 0; i < prim_count; ++i) {
         const pt_hittable& h = prims[i];
@@ -2685,7 +2492,7 @@ PT_API int pt_set_scene(pt_context* ctx, const pt_bvh_node* nodes, uint32_t node
         hp[4 * i + 3] = make_float4(u2f(h.type), 0.0f, 0.0f, 0.0f);
         hm[3 * i] = make_float4(h.base_color[0], h.base_color[1], h.base_color[2], h.roughness);
         hm[3 * i + 1] = make_float4(h.emissive[0], h.emissive[1], h.emissive[2], h.metalness);
-        hm[3 * i + 2] = make_float4(u2f(h.texture_index), u2f(h.material_type), u2f(riseFlag[i]), 0.0f);
+        hm[3 * i + 2] = make_float4(u2f(h.texture_index), u2f(h.material_type), 0.0f, 0.0f);
     }
     PT_HIP_CHECK(ctx, hipSetDevice(ctx->device));
     PT_HIP_CHECK(ctx, hipStreamSynchronize(ctx->stream));
@@ -2693,9 +2500,8 @@ PT_API int pt_set_scene(pt_context* ctx, const pt_bvh_node* nodes, uint32_t node
     (void)hipFree(ctx->prims);
     (void)hipFree(ctx->mats);
     (void)hipFree(ctx->cnodes);
-    (void)hipFree(ctx->qnodes);
-    ctx->nodes = ctx->prims = ctx->mats = ctx->cnodes = ctx->qnodes = nullptr;
-    ctx->nodeCount = ctx->primCount = ctx->cnodeCount = ctx->qnodeCount = 0;
+    ctx->nodes = ctx->prims = ctx->mats = ctx->cnodes = nullptr;
+    ctx->nodeCount = ctx->primCount = ctx->cnodeCount = 0;
     PT_HIP_CHECK(ctx, hipMalloc(&ctx->nodes, hn.size() * sizeof(float4)));
     PT_HIP_CHECK(ctx, hipMalloc(&ctx->prims, hp.size() * sizeof(float4)));
     PT_HIP_CHECK(ctx, hipMalloc(&ctx->mats, hm.size() * sizeof(float4)));
@@ -2707,12 +2513,7 @@ PT_API int pt_set_scene(pt_context* ctx, const pt_bvh_node* nodes, uint32_t node
         PT_HIP_CHECK(ctx, hipMemcpy(ctx->cnodes, hc.data(), hc.size() * sizeof(float4), hipMemcpyHostToDevice));
         ctx->cnodeCount = interior;
     }
-    if (qOk) {
-        PT_HIP_CHECK(ctx, hipMalloc(&ctx->qnodes, hq.size() * sizeof(float4)));
-        PT_HIP_CHECK(ctx, hipMemcpy(ctx->qnodes, hq.data(), hq.size() * sizeof(float4), hipMemcpyHostToDevice));
-        ctx->qnodeCount = quads;
-        ctx->qrootWord = qword(0);
-    }
+    ctx->dfsOrder = dfsOrder;
     ctx->orderStale = true;
     ctx->rootWord = word(0);
     for (int k = 0; k < 3; ++k) {
@@ -2724,14 +2525,13 @@ PT_API int pt_set_scene(pt_context* ctx, const pt_bvh_node* nodes, uint32_t node
     ctx->slabFast = slabFast;
     // LDS stack rows.  A lane visiting node v holds at most pend(v) pending entries: the ancestors
     // whose near child (trace.cu:69-76, by the sign of the ray direction along their split axis) is
-    // on the path to v -- their far child is pushed.  The walks write one entry unconditionally
-    // above the top at an interior visit (walk_interior, and the node-at-a-time walks push there),
-    // two at a 4-wide landing visit, one at a pair visit, so the rows needed are the maximum over
-    // the 8 direction octants of pend(v) + 1 over interior v (2-wide) and pend(v) + 2 over landing /
-    // pend(v) + 1 over odd-depth nodes (4-wide).  pend(v) <= depth(v) - 1, the reference's bound.
+    // on the path to v -- their far child is pushed (and repair_pending rebuilds exactly these).
+    // The walks write one entry unconditionally above the top at an interior visit (walk_interior;
+    // the node-at-a-time walks push there), so the rows needed are the maximum over the 8 direction
+    // octants of pend(v) + 1 over interior v; pend(v) <= depth(v) - 1, the reference's bound.
     {
-        std::vector<uint8_t> pend(node_count), odd(node_count, 0);
-        uint32_t need2 = 1, needQ = 1;
+        std::vector<uint8_t> pend(node_count);
+        uint32_t need = 1;
         for (uint32_t o = 0; o < 8; ++o) {
             pend[0] = 0;
             for (uint32_t i = 0; i < node_count; ++i) {
@@ -2741,13 +2541,10 @@ PT_API int pt_set_scene(pt_context* ctx, const pt_bvh_node* nodes, uint32_t node
                 const uint32_t a = i + 1, b = nodes[i].offset;
                 pend[neg ? b : a] = (uint8_t)(pend[i] + 1);
                 pend[neg ? a : b] = pend[i];
-                odd[a] = odd[b] = (uint8_t)(odd[i] ^ 1u);
-                need2 = std::max<uint32_t>(need2, pend[i] + 1u);
-                needQ = std::max<uint32_t>(needQ, pend[i] + (odd[i] ? 1u : 2u));
+                need = std::max<uint32_t>(need, pend[i] + 1u);
             }
         }
-        ctx->stackDepth = std::min(need2, maxDepth > 1 ? maxDepth - 1 : 1u);
-        ctx->qstackDepth = needQ;
+        ctx->stackDepth = std::min(need, maxDepth > 1 ? maxDepth - 1 : 1u);
     }
     return PT_OK;
 }
@@ -2790,13 +2587,11 @@ PT_API int pt_set_skybox(pt_context* ctx, uint32_t handle)
 // (1.5 tiles per slot or more: the cost-sorted list schedule balances well enough).
 static uint32_t ssg_groups(const pt_context* ctx, int variant, uint32_t tiles, uint32_t total)
 {
-    if (ctx->ssgMode == 1 || (variant != 39 && variant != 40 && variant != 41 && variant != 46 && variant != 59 &&
-                              variant != 60 && variant != 61 && variant != 66))
-        return 0;
+    if (ctx->ssgMode == 1 || (variant != 39 && variant != 40 && variant != 41 && variant != 46)) return 0;
     if (ctx->ssgMode >= 2) return std::min<uint32_t>((uint32_t)ctx->ssgMode, std::max(total, 1u));
     int cus = 0;
     if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, ctx->device) != hipSuccess) return 0;
-    const uint64_t resident = (uint64_t)cus * 4 * (variant == 46 || variant == 66 ? 4 : 5);
+    const uint64_t resident = (uint64_t)cus * 4 * (variant == 46 ? 4 : 5);
     uint64_t g = (6 * resident + tiles - 1) / tiles;
     g = std::min<uint64_t>({g, 8, total / 64});
     // measured (tools/ssg_probe.py): with 2 or 3 groups the logging, the fold and the
@@ -2820,30 +2615,6 @@ static int small_grid_variant(const pt_context* ctx, int variant, uint32_t tiles
     const size_t group = 4 * (size_t)ctx->cnodeCount * sizeof(float4) + 4 * (size_t)ctx->primCount * sizeof(float4) +
                          4 * (size_t)ctx->stackDepth * 64 * 8 + 4 * 64 * 12;
     return 4 * group <= 160 * 1024 ? 48 : 47;
-}
-
-// The 4-wide walk (walk_interior_quad) in place of the 2-wide one when the scene has the 4-wide
-// layout and its records and stacks take no more LDS per workgroup than the 2-wide ones' budget
-// (occupancy unchanged): 39 -> 59, 40 -> 60, 41 -> 61, 46 -> 66, 47 -> 67.
-constexpr bool kQuadDefault = false;
-
-static int quad_variant(const pt_context* ctx, int variant, uint32_t tiles)
-{
-    (void)tiles;
-    if (!kQuadDefault || !ctx->qnodes) return variant;
-    const size_t slices = 4 * 64 * 12;
-    const size_t q = 4 * (size_t)ctx->qstackDepth * 64 * 8 + slices;
-    const size_t c = 4 * (size_t)ctx->stackDepth * 64 * 8 + slices;
-    const size_t qRec = 8 * (size_t)ctx->qnodeCount * sizeof(float4), cRec = 4 * (size_t)ctx->cnodeCount * sizeof(float4);
-    switch (variant) {
-    case 39: case 40: case 47:                     // records staged in LDS
-        if (qRec + q > cRec + c && (qRec + q) * (variant == 47 ? 4 : 5) > 160 * 1024) return variant;
-        return variant == 39 ? 59 : (variant == 40 ? 60 : 67);
-    case 41: case 46:                              // records read through the caches
-        if (q > c && q * (variant == 46 ? 4 : 5) > 160 * 1024) return variant;
-        return variant == 41 ? 61 : 66;
-    default: return variant;
-    }
 }
 
 // Grow-only device buffers of the speculative groups; false if the device is out of memory (the
@@ -3064,15 +2835,7 @@ static int render_impl(pt_context* ctx, const pt_camera* cam, uint32_t spp, uint
     P.cam.llc = hf3(cam->lower_left_corner);
     P.cam.horizontal = hf3(cam->horizontal);
     P.cam.vertical = hf3(cam->vertical);
-    // primary rays start at the camera: in or near a sphere's box -> their t_max may rise (ChildPair)
-    P.riseAll = ctx->riseAll ? 1u : 0u;
-    P.camRise = P.riseAll;
-    for (size_t j = 0; 6 * j < ctx->sphereBoxes.size() && !P.camRise; ++j) {
-        const double* sb = &ctx->sphereBoxes[6 * j];
-        bool in = true;
-        for (int k = 0; k < 3; ++k) in = in && cam->origin[k] >= sb[k] && cam->origin[k] <= sb[3 + k];
-        P.camRise = in ? 1u : 0u;
-    }
+    P.riseAll = (ctx->riseAll || !ctx->dfsOrder) ? 1u : 0u;   // ChildPair
     P.nodeCount = ctx->nodeCount;
     P.primCount = ctx->primCount;
     P.stackDepth = ctx->stackDepth;
@@ -3080,10 +2843,6 @@ static int render_impl(pt_context* ctx, const pt_camera* cam, uint32_t spp, uint
     P.cnodes = ctx->cnodes;
     P.cnodeCount = ctx->cnodeCount;
     P.rootWord = ctx->rootWord;
-    P.qnodes = ctx->qnodes;
-    P.qnodeCount = ctx->qnodeCount;
-    P.qrootWord = ctx->qrootWord;
-    P.qstackDepth = ctx->qstackDepth;
     for (int k = 0; k < 6; ++k) P.rootBox[k] = ctx->rootBox[k];
     // Tile scheduling: a pixel's samples are sequential (one XORWOW stream), so a tile is the
     // smallest unit of work, and tiles differ several-fold in cost (sky vs geometry).  Every
@@ -3201,7 +2960,6 @@ static int render_impl(pt_context* ctx, const pt_camera* cam, uint32_t spp, uint
             (uint64_t)tiles <= (uint64_t)cus * 4 * 5)
             variant = 39;
     }
-    if (ctx->variant == 0) variant = quad_variant(ctx, variant, tiles);
     ctx->lastGroups = 0;
     memset(ctx->groupStats, 0, sizeof(ctx->groupStats));
     ++ctx->epoch;
