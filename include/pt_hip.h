@@ -239,11 +239,6 @@ PT_API int pt_set_issue_priority(pt_context *ctx, int mode, uint32_t level3, uin
  * 0 = automatic (K = 4 at <= 2 samples per pixel on large images), 1 = off, K = 2..16 = always K
  * (resumable variants).  Results are identical for every setting. */
 PT_API int pt_set_strip_units(pt_context *ctx, int mode);
-/* Check mode for a rising t_max (the sphere's far-root quirk can raise t_max mid-traversal,
- * pt_kernels.hip ChildPair): 1 = every ray keeps every far child it meets for a test at pop time
- * (the reference's rule, slower); 0 (default) = far children are kept when hit now, and the pending
- * set is rebuilt when a leaf raises t_max.  Both give the reference's results; tests compare them. */
-PT_API int pt_set_rise_check(pt_context *ctx, int all_rays);
 PT_API int pt_set_sample_groups(pt_context *ctx, int mode);
 PT_API int pt_set_patch_rounds(pt_context *ctx, uint32_t rounds);
 PT_API int pt_last_sample_groups(const pt_context *ctx);

@@ -317,12 +317,6 @@ class Pathtracer:
         for c in self._contexts():
             N.check_ctx(N.hip().pt_set_schedule(c, int(mode)), c)
 
-    def set_rise_check(self, all_rays: bool) -> None:
-        """pt_set_rise_check on every device context (True: every ray follows the reference's
-        keep-and-test-at-pop rule for far children)."""
-        for c in self._contexts():
-            N.check_ctx(N.hip().pt_set_rise_check(c, int(bool(all_rays))), c)
-
     def set_strip_units(self, mode: int) -> None:
         """pt_set_strip_units on every device context (0 automatic, 1 off, K >= 2 always K tiles per unit)."""
         for c in self._contexts():

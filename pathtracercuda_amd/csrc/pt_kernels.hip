@@ -109,8 +109,6 @@ struct TraceParams {
     uint32_t occCap;            // host only: persistent grids hold at most this many workgroups per CU (0 = all)
     uint32_t prio[3];           // issue priority by order position: < prio[0] -> 3, < prio[1] -> 2, < prio[2] -> 1
     uint32_t strip;             // MODE 3: tiles per dispatch unit (a row strip of `strip` tiles; see trace_kernel)
-    uint32_t riseAll;           // every ray keeps far children for a test at pop time (ChildPair): the check
-                                // mode pt_set_rise_check, or a BVH whose leaves are not in DFS prim order
 };
 
 // Speculative sample groups: window of a group's start offset in which an earlier group's parse can
@@ -595,19 +593,20 @@ PT_DEV float slab_lo_x(const SlabRay& R, f2v bx, f2v by, f2v bz, float tMin, flo
 // selects pick the next node, the far node and its entry distance.
 // t_max can RISE during a traversal: the sphere's far-root quirk (Hittable.inl:158, prim_hit_rec)
 // accepts t1 > t_max when t0 <= t_min, and the reference then tests the boxes it pops with that
-// larger t_max (trace.cu:48-98).  The walks keep a far child only if it is hit at the current t_max
-// (`push`) -- exact while t_max only falls -- and rebuild the pending set when a leaf raises it
-// (repair_pending).  RISEALL (wave-uniform: the check mode, or a BVH the rebuild cannot descend)
-// keeps a far child whenever its box meets the ray at all, the reference's own rule.
+// larger t_max (trace.cu:48-98).  The child-box walks keep a far child only if it is hit at the
+// current t_max (`push`) -- exact while t_max only falls -- and rebuild the pending set when a leaf
+// raises it (repair_pending).  A BVH whose leaves do not hold their primitives in DFS order (a
+// caller's, pt_set_scene) cannot be descended by the rebuild and runs the node-at-a-time walks,
+// which push every far child as the reference does.
 struct ChildPair {
-    bool push, any;             // push: keep the far child for a test at pop time; any: a child is hit
+    bool push, any;             // push: keep the far child (both children hit); any: a child is hit
     uint32_t wNext, wF;         // next node (the near one when both hit), far node
     float loNext, loF;          // their slab entry distances
 };
 
 template <bool ALLFAST = false>
 PT_DEV ChildPair cb_pair(const float4& Q0, const float4& Q1, const float4& Q2, const float4& Q3, const SlabRay& R,
-                         uint32_t negMask, float tMin, float tMax, bool riseAll)
+                         uint32_t negMask, float tMin, float tMax)
 {
     float XL, XR;
     const float loL = slab_lo_x<ALLFAST>(R, f2(Q0.x, Q0.y), f2(Q0.z, Q0.w), f2(Q1.x, Q1.y), tMin, XL);
@@ -618,7 +617,7 @@ PT_DEV ChildPair cb_pair(const float4& Q0, const float4& Q1, const float4& Q2, c
     const bool hR = XR > loR && tMax > loR;
     const bool takeL = hL && (!hR || !isNeg);
     ChildPair c;
-    c.push = riseAll ? (isNeg ? (hR && XL > loL) : (hL && XR > loR)) : (hL && hR);
+    c.push = hL && hR;
     c.any = hL || hR;
     c.wNext = takeL ? wL : wR;
     c.loNext = takeL ? loL : loR;
@@ -629,10 +628,10 @@ PT_DEV ChildPair cb_pair(const float4& Q0, const float4& Q1, const float4& Q2, c
 
 template <bool ALLFAST = false>
 PT_DEV ChildPair cb_children(const float4* __restrict__ cnodes, uint32_t cur, const SlabRay& R, uint32_t negMask,
-                             float tMin, float tMax, bool riseAll)
+                             float tMin, float tMax)
 {
     return cb_pair<ALLFAST>(cnodes[4 * cur], cnodes[4 * cur + 1], cnodes[4 * cur + 2], cnodes[4 * cur + 3], R, negMask,
-                            tMin, tMax, riseAll);
+                            tMin, tMax);
 }
 
 // The reference's pending far children at leaf `leafOff` (after a leaf raised t_max): its stack
@@ -671,11 +670,11 @@ PT_DEV void repair_pending(const float4* __restrict__ cnodes, uint2* stack, cons
 // entries -- with the stack pointer advanced only when the far child is to be kept (ChildPair).
 template <bool STATS, bool ALLFAST>
 PT_DEV bool walk_interior(const float4* __restrict__ cnodes, uint2* stack, const SlabRay& R, uint32_t negMask,
-                          float tMin, float tMax, bool riseAll, uint32_t& cur, uint32_t& sp, Counters& cnt)
+                          float tMin, float tMax, uint32_t& cur, uint32_t& sp, Counters& cnt)
 {
     while ((cur >> 24) == 0u) {
         if (STATS) { cnt.node_tests += 2; wave_tick(cnt.w_node); }
-        const ChildPair ch = cb_children<ALLFAST>(cnodes, cur, R, negMask, tMin, tMax, riseAll);
+        const ChildPair ch = cb_children<ALLFAST>(cnodes, cur, R, negMask, tMin, tMax);
         stack[64u * sp] = make_uint2(ch.wF, __float_as_uint(ch.loF));
         sp += ch.push ? 1u : 0u;
         if (ch.any) {
@@ -698,7 +697,6 @@ PT_DEV uint32_t traverse_cb(const float4* __restrict__ cnodes, const float4* __r
 {
     const float tMin = 0.001f;
     float tMax = kFltMax;
-    const bool riseAll = P.riseAll != 0u;
     SlabRay R;
     R.o = o;
     R.ix = rcp_rn(d.x);
@@ -730,7 +728,7 @@ PT_DEV uint32_t traverse_cb(const float4* __restrict__ cnodes, const float4* __r
     while (!done) {
         while ((cur >> 24) == 0u) {                               // interior walk
             if (STATS) { cnt.node_tests += 2; wave_tick(cnt.w_node); }
-            const ChildPair ch = cb_children(cnodes, cur, R, negMask, tMin, tMax, riseAll);   // trace.cu:66-77
+            const ChildPair ch = cb_children(cnodes, cur, R, negMask, tMin, tMax);   // trace.cu:66-77
             if (ch.push) {
                 stack[64u * sp] = make_uint2(ch.wF, __float_as_uint(ch.loF));
                 ++sp;
@@ -759,7 +757,8 @@ PT_DEV uint32_t traverse_cb(const float4* __restrict__ cnodes, const float4* __r
             ++leafOff;
             --leafCnt;
         }
-        if (rose && !riseAll) repair_pending(cnodes, stack, R, negMask, tMin, P.rootWord, leaf0, sp);
+        if (__ballot(rose) != 0ull && rose)                    // rare: a uniform test first
+            repair_pending(cnodes, stack, R, negMask, tMin, P.rootWord, leaf0, sp);
         if (STATS) wave_time(cnt.cyc_leaf, tPhase);
         if (!pop()) done = true;
     }
@@ -787,7 +786,6 @@ PT_DEV bool traverse_cb_phase(const float4* __restrict__ cnodes, const float4* _
                               const TraceParams& P, f3 o, f3 d, bool fresh, TravState& ts, Counters& cnt)
 {
     const float tMin = 0.001f;
-    const bool riseAll = P.riseAll != 0u;
     SlabRay R;
     R.o = o;
     R.ix = rcp_rn(d.x);
@@ -826,8 +824,8 @@ PT_DEV bool traverse_cb_phase(const float4* __restrict__ cnodes, const float4* _
     uint64_t tPhase = STATS ? __builtin_amdgcn_s_memtime() : 0;
     const bool allFast = __ballot(!R.fast) == 0;                         // wave-uniform
     while (!done) {
-        done = allFast ? walk_interior<STATS, true>(cnodes, stack, R, negMask, tMin, tMax, riseAll, cur, sp, cnt)
-                       : walk_interior<STATS, false>(cnodes, stack, R, negMask, tMin, tMax, riseAll, cur, sp, cnt);
+        done = allFast ? walk_interior<STATS, true>(cnodes, stack, R, negMask, tMin, tMax, cur, sp, cnt)
+                       : walk_interior<STATS, false>(cnodes, stack, R, negMask, tMin, tMax, cur, sp, cnt);
         if (STATS) wave_time(cnt.cyc_node, tPhase);
         if (done) break;
         uint32_t leafOff = cur & 0xffffffu, leafCnt = cur >> 24;
@@ -845,7 +843,8 @@ PT_DEV bool traverse_cb_phase(const float4* __restrict__ cnodes, const float4* _
             ++leafOff;
             --leafCnt;
         }
-        if (rose && !riseAll) repair_pending(cnodes, stack, R, negMask, tMin, P.rootWord, leaf0, sp);
+        if (__ballot(rose) != 0ull && rose)                    // rare: a uniform test first
+            repair_pending(cnodes, stack, R, negMask, tMin, P.rootWord, leaf0, sp);
         if (STATS) wave_time(cnt.cyc_leaf, tPhase);
         if (!pop()) { done = true; break; }
         // early exit once at most EXITQ/64 of the lanes that entered are still walking
@@ -1988,7 +1987,6 @@ struct pt_context {
     float4* mats = nullptr;
     float4* cnodes = nullptr;   // child-box records (traverse_cb); null when the scene exceeds its encoding
     uint32_t cnodeCount = 0, rootWord = 0;
-    bool riseAll = false;             // pt_set_rise_check
     bool dfsOrder = true;             // leaves hold their primitives in DFS order (repair_pending)
     float rootBox[6] = {};
     uint32_t nodeCount = 0, primCount = 0, stackDepth = 1;
@@ -2231,7 +2229,12 @@ constexpr uint64_t kPrepassMinSpp = 16;
 
 static int pick_variant(const pt_context* ctx)
 {
-    if (ctx->variant > 0) return ctx->variant;
+    const size_t nodeBytes = 2 * (size_t)ctx->nodeCount * sizeof(float4);
+    if (ctx->variant > 0) {
+        // a child-box walk needs leaves in DFS primitive order for repair_pending (ChildPair)
+        const bool childBox = ctx->variant != 1 && ctx->variant != 4 && ctx->variant != 6;
+        return (childBox && !ctx->dfsOrder) ? (nodeBytes <= 48 * 1024 ? 6 : 4) : ctx->variant;
+    }
     // measured on MI355X (tools/ab_variants.py, profiles/): child-box traversal (one dependent
     // fetch per interior visit, leaves inline) with while-while leaf batching and 5 waves/SIMD
     // wins on every scene; the child-box records are staged in LDS when they fit in 48 KB
@@ -2245,8 +2248,9 @@ static int pick_variant(const pt_context* ctx)
     // compiled for that occupancy (128 VGPRs, no spill), +1% on the 100k-object scene (depth 19).
     const size_t cbBytes = 4 * (size_t)ctx->cnodeCount * sizeof(float4);
     const size_t groupBytes = 4 * (size_t)ctx->stackDepth * 64 * 8 + 4 * 64 * 12;   // stacks + accumulation slices
-    if (ctx->cnodes) return cbBytes <= 48 * 1024 ? 40 : (5 * groupBytes > 160 * 1024 ? 46 : 41);
-    const size_t nodeBytes = 2 * (size_t)ctx->nodeCount * sizeof(float4);
+    // (a BVH whose leaves are not in DFS primitive order cannot be descended by repair_pending: the
+    // node-at-a-time walks, which push every far child as the reference does)
+    if (ctx->cnodes && ctx->dfsOrder) return cbBytes <= 48 * 1024 ? 40 : (5 * groupBytes > 160 * 1024 ? 46 : 41);
     return nodeBytes <= 48 * 1024 ? 6 : 4;
 }
 
@@ -2835,7 +2839,6 @@ static int render_impl(pt_context* ctx, const pt_camera* cam, uint32_t spp, uint
     P.cam.llc = hf3(cam->lower_left_corner);
     P.cam.horizontal = hf3(cam->horizontal);
     P.cam.vertical = hf3(cam->vertical);
-    P.riseAll = (ctx->riseAll || !ctx->dfsOrder) ? 1u : 0u;   // ChildPair
     P.nodeCount = ctx->nodeCount;
     P.primCount = ctx->primCount;
     P.stackDepth = ctx->stackDepth;
@@ -3048,13 +3051,6 @@ static int render_impl(pt_context* ctx, const pt_camera* cam, uint32_t spp, uint
         stats->leaf_pairs = h[20];
         stats->family_execs_compacted_in_round = h[21];
     }
-    return PT_OK;
-}
-
-PT_API int pt_set_rise_check(pt_context* ctx, int all_rays)
-{
-    if (!ctx || all_rays < 0 || all_rays > 1) return PT_ERR_ARG;
-    ctx->riseAll = all_rays != 0;
     return PT_OK;
 }
 

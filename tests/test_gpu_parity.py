@@ -644,19 +644,20 @@ def test_walk_variants_full_frame_match(gpu_available, scenes):
 @pytest.mark.parametrize("scene,W,H,calls", [("generated_scene", 1920, 1080, 16), ("test_shapes", 640, 400, 16),
                                               ("cornell_box", 512, 512, 16)])
 def test_rise_repair_matches_reference_rule(gpu_available, scenes, scene, W, H, calls):
-    # t_max rises only on rays that meet a sphere with t0 <= t_min (the far-root quirk); the walks keep
-    # a far child only if it is hit now and rebuild the reference's pending set when a leaf raises
-    # t_max (repair_pending).  With every ray under the reference's own rule (keep every far child
-    # the ray meets, test it at pop time) the bits must not change.
+    # t_max rises only on rays that meet a sphere with t0 <= t_min (the far-root quirk); the child-box
+    # walks keep a far child only if it is hit now and rebuild the reference's pending set when a
+    # leaf raises t_max (repair_pending).  Variant 1 is the reference's control flow (every far child
+    # pushed, tested when popped): the bits must be the same over many calls of whole frames
     pt = pa.Pathtracer(W, H)
     cam = pt.load_scene(scenes / f"{scene}.scene.json")
+    pt.set_strip_units(1)
     st = pt.rng_state()
     out = []
-    for all_rays in (False, True):
-        pt.set_rise_check(all_rays)
+    for variant in (0, 1):
+        pt.set_kernel_variant(variant)
         pt.set_rng_state(st)
         for i in range(calls):
             pt.render(cam, 8, i == 0)
         out.append(pt.accum().view(np.uint32).copy())
     diff = int((out[0] != out[1]).any(-1).sum())
-    assert diff == 0, f"{scene}: {diff} pixels differ from the keep-every-far-child rule"
+    assert diff == 0, f"{scene}: {diff} pixels differ from the reference's control flow"

@@ -8,7 +8,7 @@ host-built BVHs: for every ray the sequence of primitive tests must be the refer
 primitive test is a deterministic stand-in that lowers t_max, and with RISE sometimes raises it.
 Rays include axis-parallel directions (1/d infinite on two axes, the NaN-skipping slab form),
 origins on box faces and rays aimed at leaves.  The GPU parity suite checks the kernel itself bit
-for bit (and compares the rebuild against the keep-every-far-child rule, pt_set_rise_check).
+for bit (and compares the child-box walk with the reference's control flow, variant 1, over whole frames).
 """
 import pathlib
 
