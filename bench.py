@@ -146,10 +146,11 @@ def kernel_source_sha() -> str:
     import re
     h = hashlib.sha256()
     for f in ("pathtracercuda_amd/csrc/pt_kernels.hip", "pathtracercuda_amd/csrc/pt_math.h"):
-        h.update((ROOT / f).read_bytes())
+        if (ROOT / f).exists():          # (a build snapshot for A/Bs holds no sources)
+            h.update((ROOT / f).read_bytes())
     for f in sorted((ROOT / "include").glob("*.h")):
         h.update(f.read_bytes())
-    mk = (ROOT / "Makefile").read_text()
+    mk = (ROOT / "Makefile").read_text() if (ROOT / "Makefile").exists() else ""
     m = re.search(r"^HIPFLAGS \?=(.*?)(?<!\\)\n", mk, re.S | re.M)
     h.update((m.group(1) if m else "").encode())
     return h.hexdigest()[:16]

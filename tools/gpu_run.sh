@@ -63,6 +63,16 @@ for step in "$@"; do
         done
       done
       grep -o '"Msamples_s": [0-9.]*' "$O"/ab_*.log;;
+    abbench)
+      # same-box A/B of whole bench runs (C3 headline only): working tree vs $SNAP, alternating
+      for i in $(seq 1 ${PAIRS:-3}); do
+        for side in . "${SNAP:-_snap/base}"; do
+          tag=$(echo "$side" | tr '/.' 'xx')
+          (cd "$side" && timeout -k 10 300 python bench.py --steps ${STEPS:-4} --warmup 2 --secondary 0 --cpu-baseline 0 \
+              > "$O/abb_${tag}_$i.json" 2> "$O/abb_${tag}_$i.err") || { echo "FATAL abbench $side $i"; tail -5 "$O/abb_${tag}_$i.err"; exit 5; }
+          echo "$side $i $(python3 -c "import json,sys; d=json.load(open(sys.argv[1])); print(d['value'], d['ms_per_step'])" "$O/abb_${tag}_$i.json")"
+        done
+      done;;
     py:*)
       args="${step#py:}"
       echo "== python $args"
