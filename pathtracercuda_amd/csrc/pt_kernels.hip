@@ -744,19 +744,22 @@ PT_DEV uint32_t traverse_cb(const float4* __restrict__ cnodes, const float4* __r
         if (done) break;
         uint32_t leafOff = cur & 0xffffffu, leafCnt = cur >> 24;  // in-order leaf tests
         const uint32_t leaf0 = leafOff;
-        bool rose = false;
+        const float tLeaf = tMax;
         if (STATS) leaf_round_stats(prims, leafOff, leafCnt, cnt);
         while (leafCnt > 0) {
             if (STATS) { cnt.prim_tests++; wave_tick(cnt.w_prim); leaf_position_stats(prims, leafOff, cnt); }
             float t;
             if (prim_hit(prims, leafOff, o, d, tMin, tMax, t)) {
-                rose = rose || t > tMax;                          // the sphere's far-root quirk (ChildPair)
                 tMax = t;
                 elem = leafOff;
             }
             ++leafOff;
             --leafCnt;
         }
+        // t_max ended the leaf above where it started (the sphere's far-root quirk, ChildPair): boxes
+        // dropped for failing an earlier, smaller t_max may pass now.  (A rise undone within the leaf
+        // needs nothing: every dropped box failed a t_max at least as large as the one left.)
+        const bool rose = tMax > tLeaf;
         if (__ballot(rose) != 0ull && rose)                    // rare: a uniform test first
             repair_pending(cnodes, stack, R, negMask, tMin, P.rootWord, leaf0, sp);
         if (STATS) wave_time(cnt.cyc_leaf, tPhase);
@@ -830,19 +833,22 @@ PT_DEV bool traverse_cb_phase(const float4* __restrict__ cnodes, const float4* _
         if (done) break;
         uint32_t leafOff = cur & 0xffffffu, leafCnt = cur >> 24;
         const uint32_t leaf0 = leafOff;
-        bool rose = false;
+        const float tLeaf = tMax;
         if (STATS) leaf_round_stats(prims, leafOff, leafCnt, cnt);
         while (leafCnt > 0) {
             if (STATS) { cnt.prim_tests++; wave_tick(cnt.w_prim); leaf_position_stats(prims, leafOff, cnt); }
             float t;
             if (prim_hit(prims, leafOff, o, d, tMin, tMax, t)) {
-                rose = rose || t > tMax;                          // the sphere's far-root quirk (ChildPair)
                 tMax = t;
                 elem = leafOff;
             }
             ++leafOff;
             --leafCnt;
         }
+        // t_max ended the leaf above where it started (the sphere's far-root quirk, ChildPair): boxes
+        // dropped for failing an earlier, smaller t_max may pass now.  (A rise undone within the leaf
+        // needs nothing: every dropped box failed a t_max at least as large as the one left.)
+        const bool rose = tMax > tLeaf;
         if (__ballot(rose) != 0ull && rose)                    // rare: a uniform test first
             repair_pending(cnodes, stack, R, negMask, tMin, P.rootWord, leaf0, sp);
         if (STATS) wave_time(cnt.cyc_leaf, tPhase);

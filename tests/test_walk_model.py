@@ -148,14 +148,13 @@ def cb_walk(nodes, first, o, d, ray_id, rise_all=False, rebuild=True):
         n = nodes[cur]
         cnt = n.primitive_count_axis >> 16
         if cnt:
-            rose = False
+            t_leaf = tmax
             for i in range(cnt):
                 tests.append(n.offset + i)
                 t = prim_stub(n.offset + i, ray_id, tmax)
                 if t is not None:
-                    rose = rose or t > tmax
                     tmax = t
-            if rose and rebuild and not rise_all:
+            if tmax > t_leaf and rebuild and not rise_all:
                 stack[:] = repair(nodes, first, o, d, negmask, n.offset)
             cur = pop()
             continue
