@@ -1206,12 +1206,10 @@ struct SsgLane {
     uint32_t grp0;      // pos * J: the items of this tile
     uint32_t g;         // group index; G in a patch round (no window of its own)
     uint32_t k;         // samples logged
-    uint32_t d0;        // Weyl word at the item's start
-    uint32_t base;      // start offset of the item (draw pairs)
     uint32_t h;         // next group whose window this parse may reach (G: none)
     uint32_t hStart;    // its start offset
     uint32_t limit;     // samples before the item stops regardless
-    uint32_t stopOff;   // the last group stops at this draw-pair offset (~0: none)
+    // the item's start state word, start offset and (last group) stop offset: ssg_item_start
 };
 
 PT_DEV uint32_t ssg_start_word(const TraceParams& P, uint32_t item, uint32_t w, uint32_t lane)
@@ -1237,13 +1235,10 @@ PT_DEV void ssg_load(const TraceParams& P, uint32_t pos, uint32_t g, uint32_t la
         if (!(F[F_FLAG * npix + li] & 1u)) {       // finished pixel: its other fold words are stale
             sl.limit = 0;
             ps.alive = false;
-            sl.d0 = 0;
-            sl.base = 0;
             sl.h = G;
             sl.hStart = 0xffffffffu;
             return;
         }
-        sl.base = F[F_OFF * npix + li];
         rng.d = F[(F_ST + 0) * npix + li];
         rng.v0 = F[(F_ST + 1) * npix + li];
         rng.v1 = F[(F_ST + 2) * npix + li];
@@ -1264,13 +1259,10 @@ PT_DEV void ssg_load(const TraceParams& P, uint32_t pos, uint32_t g, uint32_t la
             rng.v2 = P.rng[3 * npix + li];
             rng.v3 = P.rng[4 * npix + li];
             rng.v4 = P.rng[5 * npix + li];
-            sl.base = 0;
         } else {
-            sl.base = ssg_start_word(P, sl.logItem, 0, lane);
-            if (sl.base == 0xffffffffu) {          // the second phase of a pixel that has none
+            if (ssg_start_word(P, sl.logItem, 0, lane) == 0xffffffffu) {   // the second phase of a pixel that has none
                 sl.limit = 0;
                 ps.alive = false;
-                sl.d0 = 0;
                 sl.h = G;
                 sl.hStart = 0xffffffffu;
                 return;
@@ -1288,10 +1280,31 @@ PT_DEV void ssg_load(const TraceParams& P, uint32_t pos, uint32_t g, uint32_t la
         sl.h = g + 1;
         sl.limit = P.ssgCap;
     }
-    sl.d0 = rng.d;
     sl.hStart = sl.h < G ? ssg_start_word(P, sl.grp0 + 2 * sl.h - 1, 0, lane) : 0xffffffffu;
-    sl.stopOff = (!P.ssgPatch && sl.g + 1 == G) ? ssg_start_word(P, sl.logItem, 7, lane) : 0xffffffffu;
     ps.alive = sl.limit > 0;
+}
+
+// The item's start (Weyl word d0, draw-pair offset base) and, for the last group, its stop offset:
+// constant for the whole item, so they are re-read from the start records (L1/L2) when a sample
+// ends instead of being held in registers across the kernel's loop (they pushed the grouped
+// instantiation into spills).
+PT_DEV void ssg_item_start(const TraceParams& P, const SsgLane& sl, uint32_t lane, size_t li, uint32_t& d0, uint32_t& base,
+                           uint32_t& stopOff)
+{
+    const size_t npix = (size_t)P.rows * P.width;
+    if (P.ssgPatch) {
+        d0 = P.fold[(F_ST + 0) * npix + li];
+        base = P.fold[F_OFF * npix + li];
+        stopOff = 0xffffffffu;
+    } else if (sl.g == 0) {
+        d0 = P.rng[li];
+        base = 0;
+        stopOff = sl.g + 1 == P.ssgG ? ssg_start_word(P, sl.logItem, 7, lane) : 0xffffffffu;
+    } else {
+        d0 = ssg_start_word(P, sl.logItem, 1, lane);
+        base = ssg_start_word(P, sl.logItem, 0, lane);
+        stopOff = sl.g + 1 == P.ssgG ? ssg_start_word(P, sl.logItem, 7, lane) : 0xffffffffu;
+    }
 }
 
 // End of a path in a speculative item: log it, record the sample start that follows (in the group's
@@ -1299,22 +1312,24 @@ PT_DEV void ssg_load(const TraceParams& P, uint32_t pos, uint32_t g, uint32_t la
 // sample.
 template <bool STATS>
 PT_DEV void ssg_finish(const TraceParams& P, PathState& ps, Xorwow& rng, float fx, float fy, SsgLane& sl,
-                       uint32_t lane, Counters& cnt)
+                       uint32_t lane, size_t li, Counters& cnt)
 {
+    uint32_t d0, base, stopOff;
+    ssg_item_start(P, sl, lane, li, d0, base, stopOff);
     if (STATS) cnt.samples++;
     const size_t rec = (size_t)sl.logItem * P.ssgCap + sl.k;
     P.ssgLog[(rec * 3 + 0) * 64 + lane] = ps.L.x;
     P.ssgLog[(rec * 3 + 1) * 64 + lane] = ps.L.y;
     P.ssgLog[(rec * 3 + 2) * 64 + lane] = ps.L.z;
-    const uint32_t rel = ((rng.d - sl.d0) * kInvWeyl) >> 1;          // draw pairs since the item's start
+    const uint32_t rel = ((rng.d - d0) * kInvWeyl) >> 1;             // draw pairs since the item's start
     P.ssgEnd[rec * 64 + lane] = (uint16_t)rel;
     ++sl.k;
     bool stop = sl.k >= sl.limit;
     if (sl.g - 1u < P.ssgG - 1u && rel < (P.ssgWin * 64u))                    // groups 1 .. G-1
         __hip_atomic_fetch_or(&P.ssgBits[((size_t)sl.logItem * P.ssgWin + rel / 64) * 64 + lane], 1ull << (rel % 64),
                               __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    const uint32_t off = sl.base + rel;
-    stop = stop || off >= sl.stopOff;                                  // the last group: past the expected end
+    const uint32_t off = base + rel;
+    stop = stop || off >= stopOff;                                     // the last group: past the expected end
     const uint32_t j = sl.logItem - sl.grp0;
     if (!stop && j >= 2 && !(j & 1u) && !P.ssgPatch && rel + 1 < (P.ssgWin * 64u)) {
         // the second phase has joined the first one's parse (a sample start of item j - 1): from here
@@ -1534,7 +1549,7 @@ __global__ void __launch_bounds__(WPB * 64, MINW) trace_kernel(TraceParams P)
                 if (!tdone) continue;                              // suspended: resumes next round
                 uint64_t tS = STATS ? __builtin_amdgcn_s_memtime() : 0;
                 if (shade<STATS>(P, prims, ts.elem, ts.tMax, ps, rng, cnt)) {
-                    if (SSG) ssg_finish<STATS>(P, ps, rng, fx, fy, sl, lane, cnt);
+                    if (SSG) ssg_finish<STATS>(P, ps, rng, fx, fy, sl, lane, pc.li, cnt);
                     else finish_path<STATS>(P, ps, rng, fx, fy, cnt);
                     if (STRIP && !ps.alive && stripK + 1 < P.strip) {
                         // Strip units (launches of few samples per pixel): a lane whose pixel is done
@@ -1565,7 +1580,7 @@ __global__ void __launch_bounds__(WPB * 64, MINW) trace_kernel(TraceParams P)
                                        : traverse<STATS, WW>(nodes, prims, stack, ps.o, ps.d, P.slabFast != 0, t, cnt);
             uint64_t tS = STATS ? __builtin_amdgcn_s_memtime() : 0;
             if (shade<STATS>(P, prims, e, t, ps, rng, cnt)) {
-                if (SSG) ssg_finish<STATS>(P, ps, rng, fx, fy, sl, lane, cnt);
+                if (SSG) ssg_finish<STATS>(P, ps, rng, fx, fy, sl, lane, pc.li, cnt);
                 else finish_path<STATS>(P, ps, rng, fx, fy, cnt);
             }
             if (STATS) wave_time(cnt.cyc_shade, tS);
