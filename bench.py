@@ -82,6 +82,8 @@ def parse_args(argv=None):
     p.add_argument("--cpu-baseline", type=int, default=1, help="time the oracle on a bounded sample (rank 0, N=1)")
     p.add_argument("--cpu-seconds", type=float, default=15.0, help="target length of the CPU baseline run")
     p.add_argument("--cpu-threads", type=int, default=0, help="0 = every core this process may use")
+    p.add_argument("--call-loop", type=int, default=1,
+                   help="N=1, C3: also time the reference's unchanged 128-call loop (secondary record)")
     p.add_argument("--extra", default="C5", help="N=1: secondary records after C2 (comma-separated labels; '' = none)")
     p.add_argument("--group", type=int, default=-1,
                    help="in-process device group (pt_group_*): 1 = always, 0 = never, -1 = when --gpus > 1 "
@@ -494,7 +496,7 @@ def main():
     if args.secondary:
         if n == 1:
             recs = []
-            if args.config == "C3":
+            if args.config == "C3" and args.call_loop:
                 # the reference's unchanged call loop on the headline workload
                 rl = CallLoopRun(cfg, W, H, spp, 0, 1, local_rank, 1, "single")
                 el, kl = timed(rl, args.steps, args.warmup, local_rank, False, use_torch)

@@ -6,7 +6,8 @@
 #   tests        pytest -m gpu (thread timeouts, one process)
 #   smoke        __graft_entry__.smoke()
 #   bench        python bench.py $BENCH_ARGS                      -> $O/bench.json
-#   kprof        rocprofv3 --kernel-trace --stats of the bench     -> $O/prof_bench/
+#   kprof        rocprofv3 --kernel-trace --stats of the bench (headline + C2 only, so the
+#                headline kernel's average is its timed launches') -> $O/prof_bench/
 #   pmc          rocprofv3 --pmc passes (one counter group per run) of the timed launches of the
 #                workloads in $PMC (default "c3 c2 c5")            -> $O/pmc_<w>/p<i>/
 #   ab           same-box A/B of the working tree against the snapshot $SNAP (tools/snap_rev.sh),
@@ -36,7 +37,7 @@ for step in "$@"; do
       rc=$?; tail -c 400 "$O/bench.json"; echo; fatal $rc bench;;
     kprof)
       echo "== rocprofv3 kernel trace"
-      (cd /tmp && timeout -k 10 600 rocprofv3 --kernel-trace --stats -d "$O/prof_bench" -o run --output-format csv -- python3 "$R/bench.py" --cpu-baseline 0 --extra '') > "$O/prof_bench.log" 2>&1
+      (cd /tmp && timeout -k 10 600 rocprofv3 --kernel-trace --stats -d "$O/prof_bench" -o run --output-format csv -- python3 "$R/bench.py" --cpu-baseline 0 --call-loop 0 --extra '') > "$O/prof_bench.log" 2>&1
       rc=$?; tail -1 "$O/prof_bench.log"; fatal $rc rocprof;;
     pmc)
       i=0

@@ -45,6 +45,14 @@ for mode in (1, a.groups):
                   "stats": pt.group_stats()})
         by_g = [round(float(c[:, g][c[:, g] > 0].mean()) / nom, 3) if (c[:, g] > 0).any() else 0 for g in range(2 * G - 1)]
         r["mean_count_by_group"] = by_g
+        # slot time in samples: an item holds its wave slot for its slowest lane's count; dead lanes
+        # (no second phase, stopped early) idle beside it
+        live = [round(float((c[:, j] > 0).mean()), 3) for j in range(2 * G - 1)]
+        eff = [round(float(c[:, j].sum()) / max(1.0, float(64 * c[:, j].max(-1).sum())), 3) for j in range(2 * G - 1)]
+        r["live_lane_frac_by_item"] = live
+        r["slot_efficiency_by_item"] = eff
+        r["slot_efficiency"] = round(float(c.sum()) / float(64 * itemmax.sum()), 3)
+        r["slot_samples_over_needed"] = round(float(64 * itemmax.sum()) / (pt.rows * a.width * a.spp), 3)
     res["groups" if mode != 1 else "plain"] = r
     print(json.dumps(r), flush=True)
     pt.close()
