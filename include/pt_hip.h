@@ -233,7 +233,11 @@ PT_API int pt_set_issue_priority(pt_context *ctx, int mode, uint32_t level3, uin
  * after fold rounds 0..7.  pt_read_group_log_counts: samples each (tile, item) logged per lane
  * ([tile][2G - 1][64], tiles in dispatch (cost) order; item 0 = group 0, items 2g - 1 and 2g =
  * group g at its guessed offset and one draw pair later).  pt_set_patch_rounds: patch rounds before
- * the remaining dead ends run as a plain resume launch (default 6; 0 exercises the resume path). */
+ * the remaining dead ends run as a plain resume launch (default 6; 0 exercises the resume path).
+ * pt_set_group_lookback: a second phase (the item one pair later) also stops where its first
+ * phase's parse holds the second phase's sample start `far` or `near` samples back -- the first
+ * phase may run behind on the parse the two share (defaults 64 and 16; 0 = off: only the current
+ * start).  Scheduling only: results are identical for every setting. */
 /* Tuning knob: tiles per dispatch unit of launches with few samples per pixel (a row strip of K
  * tiles; a lane whose pixel is done takes the same position in the next tile of its strip).
  * 0 = automatic (K = 4 at <= 2 samples per pixel on large images), 1 = off, K = 2..16 = always K
@@ -241,6 +245,7 @@ PT_API int pt_set_issue_priority(pt_context *ctx, int mode, uint32_t level3, uin
 PT_API int pt_set_strip_units(pt_context *ctx, int mode);
 PT_API int pt_set_sample_groups(pt_context *ctx, int mode);
 PT_API int pt_set_patch_rounds(pt_context *ctx, uint32_t rounds);
+PT_API int pt_set_group_lookback(pt_context *ctx, uint32_t far, uint32_t near);
 PT_API int pt_last_sample_groups(const pt_context *ctx);
 PT_API int pt_read_group_stats(const pt_context *ctx, uint32_t *dst);
 PT_API int pt_read_group_log_counts(pt_context *ctx, uint32_t *dst, size_t count);

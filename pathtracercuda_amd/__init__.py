@@ -336,6 +336,12 @@ class Pathtracer:
         for c in self._contexts():
             N.check_ctx(N.hip().pt_set_patch_rounds(c, int(rounds)), c)
 
+    def set_group_lookback(self, far: int = 64, near: int = 16) -> None:
+        """Sample groups: a second phase also stops on a junction with its first phase `far` or
+        `near` samples back (0 = off).  Scheduling only (pt_set_group_lookback)."""
+        for c in self._contexts():
+            N.check_ctx(N.hip().pt_set_group_lookback(c, int(far), int(near)), c)
+
     def group_fold_word(self, word: int) -> np.ndarray:
         """Diagnostics: a plane of the grouped launch's fold state (pt_read_group_fold); word 19 =
         draw pairs per sample (float32)."""

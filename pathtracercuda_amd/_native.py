@@ -83,6 +83,7 @@ _HIP_SYMBOLS = {
     "pt_last_sample_groups": (C.c_int, [C.c_void_p]),
     "pt_read_group_stats": (C.c_int, [C.c_void_p, P(C.c_uint32)]),
     "pt_set_patch_rounds": (C.c_int, [C.c_void_p, C.c_uint32]),
+    "pt_set_group_lookback": (C.c_int, [C.c_void_p, C.c_uint32, C.c_uint32]),
     "pt_read_group_fold": (C.c_int, [C.c_void_p, C.c_uint32, P(C.c_uint32)]),
     "pt_read_group_log_counts": (C.c_int, [C.c_void_p, P(C.c_uint32), C.c_size_t]),
     "pt_last_error": (C.c_char_p, [C.c_void_p]),

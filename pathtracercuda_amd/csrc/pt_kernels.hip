@@ -104,6 +104,8 @@ struct TraceParams {
     unsigned long long* ssgBits;// [item][ssgWin][64] the item's sample starts in its window
     uint32_t ssgWin;            // window words per lane (64 draw pairs each) after an item's start
     uint32_t* ssgCount;         // [item][64] samples logged
+    uint32_t ssgLook[2];        // a second phase also stops where its first phase's parse holds its
+                                // sample start this many samples back (lag tolerance; 0 = off)
     uint32_t* fold;             // [kFoldWords][rows*width] fold state (ssg_fold_kernel); AUX resume input
     DevCamera cam;
     uint32_t occCap;            // host only: persistent grids hold at most this many workgroups per CU (0 = all)
@@ -1335,8 +1337,19 @@ PT_DEV void ssg_finish(const TraceParams& P, PathState& ps, Xorwow& rng, float f
         // the second phase has joined the first one's parse (a sample start of item j - 1): from here
         // the two are the same parse, the first carries on
         const uint32_t wa = rel + 1;
-        stop = (__hip_atomic_load(&P.ssgBits[((size_t)(sl.logItem - 1) * P.ssgWin + wa / 64) * 64 + lane], __ATOMIC_RELAXED,
-                                  __HIP_MEMORY_SCOPE_AGENT) >> (wa % 64)) & 1ull;
+        const unsigned long long* bitsA = P.ssgBits + (size_t)(sl.logItem - 1) * P.ssgWin * 64 + lane;
+        stop = (__hip_atomic_load(&bitsA[(wa / 64) * 64], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) >> (wa % 64)) & 1ull;
+        // the first phase may run behind on the parse the two share: a start ssgLook samples back
+        // that it holds means the two coincide from there (the fold continues in its log)
+#pragma unroll
+        for (int q = 0; q < 2; ++q) {
+            const uint32_t L = P.ssgLook[q];
+            if (!stop && L && sl.k > L) {
+                const uint32_t wb = (uint32_t)P.ssgEnd[(rec - L) * 64 + lane] + 1u;
+                stop = wb < (P.ssgWin * 64u) &&
+                       ((__hip_atomic_load(&bitsA[(wb / 64) * 64], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) >> (wb % 64)) & 1ull);
+            }
+        }
     }
     while (sl.h < P.ssgG && off > sl.hStart + (P.ssgWin * 64u)) {           // passed that group's windows
         ++sl.h;
@@ -2043,6 +2056,7 @@ struct pt_context {
     // speculative sample groups
     int ssgMode = 0;              // 0 = automatic, 1 = off, G >= 2 = always G groups (tests)
     uint32_t patchRounds = 6;     // patch rounds before the remaining dead ends run plain
+    uint32_t ssgLook[2] = {64, 16}; // second-phase lag tolerances in samples (TraceParams::ssgLook)
     float* pairs = nullptr;       // per-pixel draw pairs per sample (start-offset guesses)
     bool pairsValid = false;
     uint32_t* ssgStart = nullptr;
@@ -2765,6 +2779,8 @@ static int run_groups(pt_context* ctx, int variant, const TraceParams& P0, uint3
     PT_HIP_CHECK(ctx, hipMemsetAsync(ctx->deadCount, 0, sizeof(uint32_t), s));
     ssg_guess_kernel<<<pixBlocks, 256, 0, s>>>(P, ctx->pairs, ssgN, ctx->ssgStart);
     PT_HIP_CHECK(ctx, hipGetLastError());
+    P.ssgLook[0] = ctx->ssgLook[0];
+    P.ssgLook[1] = ctx->ssgLook[1];
     PT_HIP_CHECK(ctx, launch_grouped<1>(variant, P, s));
     ssg_fold_kernel<<<pixBlocks, 256, 0, s>>>(P, 0, ctx->patchLog, ctx->patchEnd, ctx->patchCount, ssgCap, ctx->pairs,
                                               ctx->deadCount);
@@ -3086,6 +3102,14 @@ PT_API int pt_set_sample_groups(pt_context* ctx, int mode)
 {
     if (!ctx || mode < 0 || mode > 4096) return PT_ERR_ARG;
     ctx->ssgMode = mode;
+    return PT_OK;
+}
+
+PT_API int pt_set_group_lookback(pt_context* ctx, uint32_t far, uint32_t near)
+{
+    if (!ctx || far > 256 || near > 256) return PT_ERR_ARG;
+    ctx->ssgLook[0] = far;
+    ctx->ssgLook[1] = near;
     return PT_OK;
 }
 

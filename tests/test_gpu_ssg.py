@@ -81,6 +81,30 @@ def test_groups_equal_plain_launch_patch_and_resume(gpu_available, scenes, round
         assert st["patch_rounds"] >= 1, st
 
 
+@pytest.mark.parametrize("groups", [2, 4])
+def test_group_lookback_bitexact(gpu_available, scenes, groups):
+    """The second phases' lag tolerance (pt_set_group_lookback) is scheduling only: every setting
+    gives the plain launch's bits, on a rank share (ground pixels: many second phases) and on a
+    ragged image."""
+    for W, H, kw, name in ((1920, 1080, dict(row_offset=5, row_stride=8, band_rows=8), "generated_scene"),
+                           (37, 21, {}, "cornell_box")):
+        p = str(scenes / f"{name}.scene.json")
+        out = {}
+        for cfg in ("plain", (0, 0), (1, 0), (8, 0), (32, 8), (256, 3)):
+            pt = pa.Pathtracer(W, H, **kw)
+            cam = pt.load_scene(p)
+            pt.set_sample_groups(1 if cfg == "plain" else groups)
+            if cfg != "plain":
+                pt.set_group_lookback(*cfg)
+            pt.render(cam, 8, True, chunks=16)
+            assert pt.last_sample_groups == (0 if cfg == "plain" else groups)
+            out[cfg] = (pt.accum(), pt.rng_state())
+            pt.close()
+        for cfg, (acc, st) in out.items():
+            same(acc, out["plain"][0], f"{name} G={groups} lookback {cfg}")
+            assert np.array_equal(st, out["plain"][1]), cfg
+
+
 def test_groups_refused_beyond_the_fold_word(gpu_available, scenes):
     # ADVICE r02: the fold state packs (sample in call, call) as sIdx | c << 16, so a launch of more
     # than 65,535 render() calls (or spp) must not run grouped; forced groups then run plain and the

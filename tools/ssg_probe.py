@@ -22,11 +22,17 @@ ap.add_argument("--n", type=int, default=8)
 ap.add_argument("--rank", type=int, default=0)
 ap.add_argument("--groups", type=int, default=0, help="0 = automatic, G >= 2 forced")
 ap.add_argument("--scene", default=str(ROOT / "scenes/generated_scene.scene.json"))
+ap.add_argument("--lookback", default="d",
+                help="comma-separated far:near second-phase lookbacks of the grouped runs (set_group_lookback; "
+                     "'d' = the library's default)")
 a = ap.parse_args()
 res = {"image": f"{a.width}x{a.height}", "spp": a.spp, "n": a.n, "rank": a.rank}
-for mode in (1, a.groups):
+runs = [("plain", 1, "d")] + [("groups" if cfg == "d" else f"groups_look{cfg}", a.groups, cfg) for cfg in a.lookback.split(",")]
+for name, mode, cfg in runs:
     pt = pa.Pathtracer(a.width, a.height, row_offset=a.rank, row_stride=a.n, band_rows=8)
     pt.set_sample_groups(mode)
+    if cfg != "d":
+        pt.set_group_lookback(*(int(x) for x in cfg.split(":")))
     cam = pt.load_scene(a.scene)
     pt.render_raw(cam, 8, a.spp // 8, True)
     ms = [pt.render_raw(cam, 8, a.spp // 8, True) for _ in range(2)]
@@ -53,7 +59,7 @@ for mode in (1, a.groups):
         r["slot_efficiency_by_item"] = eff
         r["slot_efficiency"] = round(float(c.sum()) / float(64 * itemmax.sum()), 3)
         r["slot_samples_over_needed"] = round(float(64 * itemmax.sum()) / (pt.rows * a.width * a.spp), 3)
-    res["groups" if mode != 1 else "plain"] = r
+    res[name] = r
     print(json.dumps(r), flush=True)
     pt.close()
 print(json.dumps(res))
