@@ -250,8 +250,8 @@ PT_API int pt_last_sample_groups(const pt_context *ctx);
 PT_API int pt_read_group_stats(const pt_context *ctx, uint32_t *dst);
 PT_API int pt_read_group_log_counts(pt_context *ctx, uint32_t *dst, size_t count);
 /* Diagnostics: one word plane of the per-pixel fold state (rows x width; word 16 = dead-end flag,
- * 7 = samples done, 8 = draw-pair offset), or with word 19 the draw pairs per sample (float) that
- * the next launch's guesses use. */
+ * 7 = samples done, 8 = draw-pair offset), or with words 19 / 20 / 21 the statistics the next
+ * launch's guesses use (float): draw pairs per sample, odd-length fraction, variance. */
 PT_API int pt_read_group_fold(pt_context *ctx, uint32_t word, uint32_t *dst);
 PT_API const char *pt_last_error(const pt_context *ctx);
 

@@ -343,12 +343,12 @@ class Pathtracer:
             N.check_ctx(N.hip().pt_set_group_lookback(c, int(far), int(near)), c)
 
     def group_fold_word(self, word: int) -> np.ndarray:
-        """Diagnostics: a plane of the grouped launch's fold state (pt_read_group_fold); word 19 =
-        draw pairs per sample (float32)."""
+        """Diagnostics: a plane of the grouped launch's fold state (pt_read_group_fold); words 19 /
+        20 / 21 = the guess statistics (float32): draw pairs per sample, odd-length fraction, variance."""
         self._single("group_fold_word")
         out = np.zeros((self.rows, self.width), dtype=np.uint32)
         N.check_ctx(N.hip().pt_read_group_fold(self._ctx, int(word), out.ctypes.data_as(C.POINTER(C.c_uint32))), self._ctx)
-        return out.view(np.float32) if word == 19 else out
+        return out.view(np.float32) if word >= 19 else out
 
     def group_stats(self) -> Dict[str, object]:
         """How the last grouped launch went: groups, patch rounds, dead-end pixels after each fold."""

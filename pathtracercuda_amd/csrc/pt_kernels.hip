@@ -1355,6 +1355,14 @@ PT_DEV void ssg_finish(const TraceParams& P, PathState& ps, Xorwow& rng, float f
         ++sl.h;
         sl.hStart = sl.h < P.ssgG ? ssg_start_word(P, sl.grp0 + 2 * sl.h - 1, 0, lane) : 0xffffffffu;
     }
+    // reached the next group's start without meeting group h (the windows overlap the following
+    // groups): the candidate becomes the latest group started, whose two phases are still fresh
+    while (sl.h + 1 < P.ssgG) {
+        const uint32_t nx = ssg_start_word(P, sl.grp0 + 2 * sl.h + 1, 0, lane);
+        if (off < nx) break;
+        ++sl.h;
+        sl.hStart = nx;
+    }
     if (!stop && sl.h < P.ssgG && off >= sl.hStart) {
         // junction: a sample start of group h's parse (either phase; an idle phase has no bits)
         const uint32_t w = off - sl.hStart;
@@ -1819,6 +1827,12 @@ __global__ void __launch_bounds__(256) ssg_fold_kernel(TraceParams P, uint32_t r
             ++h;
             hStart = h < G ? ssg_start_word(P, item0 + 2 * h - 1, 0, lane) : 0xffffffffu;
         }
+        while (h + 1 < G) {                                  // the latest group started (ssg_finish)
+            const uint32_t nx = ssg_start_word(P, item0 + 2 * h + 1, 0, lane);
+            if (off < nx) break;
+            ++h;
+            hStart = nx;
+        }
         if (h < G && off >= hStart) {
             bool joined = false;
             for (uint32_t ph = 0; ph < 2 && !joined; ++ph) {        // both phases of group h
@@ -1900,11 +1914,13 @@ __global__ void __launch_bounds__(256) ssg_fold_kernel(TraceParams P, uint32_t r
                 const unsigned long long word = idx == i ? w0 : (idx == i + 1 ? w1 : (idx < P.ssgWin ? b[idx * 64] : 0ull));
                 return (word >> (w % 64)) & 1ull;
             };
+            const uint32_t hNext = h + 1 < G ? ssg_start_word(P, item0 + 2 * h + 1, 0, lane) : 0xffffffffu;
             for (uint32_t j = 0; j + 1 < m; ++j) {
                 const uint32_t pos = base + er[j];
                 if (pos < hStart) continue;
                 const uint32_t w = pos - hStart;
-                if (w > (P.ssgWin * 64u) || (w < (P.ssgWin * 64u) && bit(a0, a1, i0, bA, w)) || (w >= 1 && bit(c0, c1, iB, bB, w - 1))) {
+                if (w > (P.ssgWin * 64u) || pos >= hNext || (w < (P.ssgWin * 64u) && bit(a0, a1, i0, bA, w)) ||
+                    (w >= 1 && bit(c0, c1, iB, bB, w - 1))) {
                     m = j + 1;
                     break;
                 }
@@ -1964,7 +1980,7 @@ __global__ void __launch_bounds__(256) ssg_fold_kernel(TraceParams P, uint32_t r
             const float mean = (float)off / (float)done;
             pairs[2 * npix + li] = fmaxf((float)sq / (float)done - mean * mean, 0.0f);
         }
-        F[F_FLAG * npix + li] = 0u;
+        F[F_FLAG * npix + li] = round << 8;      // finished (bit 0 clear), in this fold round (diagnostics)
         return;
     }
     if (done > 0) pairs[li] = (float)off / (float)done;   // the next launch's guess for this pixel
@@ -3139,11 +3155,12 @@ PT_API int pt_read_group_log_counts(pt_context* ctx, uint32_t* dst, size_t count
 
 PT_API int pt_read_group_fold(pt_context* ctx, uint32_t word, uint32_t* dst)
 {
-    if (!ctx || !dst || word >= kFoldWords + 1) return PT_ERR_ARG;
+    if (!ctx || !dst || word >= kFoldWords + 3) return PT_ERR_ARG;
     if (!ctx->fold) return PT_ERR_STATE;
     PT_HIP_CHECK(ctx, hipSetDevice(ctx->device));
     const size_t npix = (size_t)ctx->rows * ctx->width;
-    const void* src = word == kFoldWords ? (const void*)ctx->pairs : (const void*)(ctx->fold + (size_t)word * npix);
+    const void* src = word >= kFoldWords ? (const void*)(ctx->pairs + (word - kFoldWords) * npix)
+                                         : (const void*)(ctx->fold + (size_t)word * npix);
     PT_HIP_CHECK(ctx, hipMemcpy(dst, src, npix * sizeof(uint32_t), hipMemcpyDeviceToHost));
     return PT_OK;
 }

@@ -22,6 +22,7 @@ ap.add_argument("--n", type=int, default=8)
 ap.add_argument("--rank", type=int, default=0)
 ap.add_argument("--groups", type=int, default=0, help="0 = automatic, G >= 2 forced")
 ap.add_argument("--scene", default=str(ROOT / "scenes/generated_scene.scene.json"))
+ap.add_argument("--reps", type=int, default=2, help="timed launches after the cold one")
 ap.add_argument("--lookback", default="d",
                 help="comma-separated far:near second-phase lookbacks of the grouped runs (set_group_lookback; "
                      "'d' = the library's default)")
@@ -35,8 +36,11 @@ for name, mode, cfg in runs:
         pt.set_group_lookback(*(int(x) for x in cfg.split(":")))
     cam = pt.load_scene(a.scene)
     pt.render_raw(cam, 8, a.spp // 8, True)
-    ms = [pt.render_raw(cam, 8, a.spp // 8, True) for _ in range(2)]
-    r = {"ms": [round(x, 2) for x in ms], "groups": pt.last_sample_groups}
+    ms, st = [], []
+    for _ in range(a.reps):
+        ms.append(pt.render_raw(cam, 8, a.spp // 8, True))
+        st.append(pt.group_stats() if pt.last_sample_groups else None)
+    r = {"ms": [round(x, 2) for x in ms], "groups": pt.last_sample_groups, "stats_by_rep": st}
     if pt.last_sample_groups:
         G = pt.last_sample_groups
         nom = a.spp // G
