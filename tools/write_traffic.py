@@ -16,9 +16,14 @@ def main():
     tag = sys.argv[2] if len(sys.argv) > 2 else "r01"
     workload = sys.argv[3] if len(sys.argv) > 3 else "generated_scene 1920x1080 1024spp chunk8"
     disp, names = load(src, "trace_kernel<false")
-    best = {}
+    # per pass directory the timed launch: the LAST dispatch at least half as long as the longest (the
+    # warm-up launch comes first; it rebuilds the cost order and runs without issue priority)
+    longest = {}
     for (p, i), c in disp.items():
-        if p not in best or c.get("DURATION_NS", 0) > best[p].get("DURATION_NS", 0):
+        longest[p] = max(longest.get(p, 0.0), c.get("DURATION_NS", 0))
+    best = {}
+    for (p, i), c in sorted(disp.items()):
+        if c.get("DURATION_NS", 0) >= 0.5 * longest[p]:
             best[p] = c
     merged = {}
     for p, c in sorted(best.items()):
