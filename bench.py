@@ -25,8 +25,9 @@ samples / the slowest rank's step time.  At N > 1 a weak-scaling record is added
 (`secondary`: every GPU keeps one C3 frame's worth of pixels, the image grows by sqrt(N) per axis),
 so both are on the driver's clock; `--scaling weak` swaps them.  At N = 1 the two coincide, and the
 secondary records are the reference's unchanged call loop on C3 (128 separate render(cam, 8, i == 0)
-calls through the drop-in Pathtracer, main.cpp:272-279), C2 and C5, each C2/C5 with its roofline and
-CPU baseline (`--extra ''` drops C5, `--secondary 0` turns all secondary records off).
+calls through the drop-in Pathtracer, main.cpp:272-279), a cold one-shot C3 render (fresh context,
+cost pre-pass included), C2 and C5, each C2/C5 with its roofline and CPU baseline (`--extra ''` drops
+C5, `--secondary 0` turns all secondary records off).
 
 Printed JSON line (rank 0): value = samples of the whole workload / step time.  roofline: the
 trace kernel is bound by VALU issue -- achieved = its wave64 VALU instructions per
@@ -84,6 +85,8 @@ def parse_args(argv=None):
     p.add_argument("--cpu-threads", type=int, default=0, help="0 = every core this process may use")
     p.add_argument("--call-loop", type=int, default=1,
                    help="N=1, C3: also time the reference's unchanged 128-call loop (secondary record)")
+    p.add_argument("--cold", type=int, default=1,
+                   help="N=1, C3: also time a cold one-shot render (fresh context, pre-pass included; secondary record)")
     p.add_argument("--extra", default="C5", help="N=1: secondary records after C2 (comma-separated labels; '' = none)")
     p.add_argument("--group", type=int, default=-1,
                    help="in-process device group (pt_group_*): 1 = always, 0 = never, -1 = when --gpus > 1 "
@@ -313,6 +316,33 @@ class CallLoopRun(Run):
         return total
 
 
+def cold_one_shot(cfg, W, H, spp, local_rank, warm_step_s, use_torch, reps=3):
+    """A one-shot render the way `pathtracer -w W -h H -spp SPP` runs it (main.cpp:262-295): a fresh
+    context (Pathtracer ctor, scene load: untimed), then ONE render of the whole workload with no tile
+    costs yet -- the built-in cost pre-pass, its sort and the launch in the pre-pass's order, all
+    inside the timed call.  `reps` fresh contexts; the kernel module is already loaded in this process."""
+    import pathtracercuda_amd as pa
+    walls, gpus = [], []
+    for _ in range(reps):
+        pt = pa.Pathtracer(W, H, device=local_rank)
+        cam = pt.load_scene(scene_path(cfg["scene"]))
+        if use_torch:
+            import torch
+            torch.cuda.synchronize(local_rank)
+        t0 = time.perf_counter()
+        gpus.append(pt.render_raw(cam, CHUNK, spp // CHUNK, True))
+        walls.append(time.perf_counter() - t0)
+        pt.close()
+    med = sorted(walls)[len(walls) // 2]
+    return {"label": "C3 cold one-shot", "value": round(W * H * spp / med / 1e6, 3), "unit": "Msamples/s",
+            "ms_per_step": round(med * 1e3, 3), "runs_ms": [round(w * 1e3, 3) for w in walls],
+            "gpu_ms": [round(g, 3) for g in gpus], "cold_over_warm": round(med / warm_step_s, 4),
+            "workload": workload_name(cfg, W, H, spp) + ", first launch of a fresh context",
+            "what": "fresh Pathtracer + scene load (untimed), then one render_raw of the whole workload: cost "
+                    "pre-pass + device sort + the launch in that order (wall time of the call; median of "
+                    f"{reps} fresh contexts); cold_over_warm = its time / the headline's step time"}
+
+
 def timed(run, steps, warmup, local_rank, dist_on, use_torch=True):
     if not use_torch:
         # the in-process device group (main): pt_group_render / pt_group_gather return after every
@@ -351,7 +381,7 @@ def timed(run, steps, warmup, local_rank, dist_on, use_torch=True):
 
 LANE_KEYS = ("node_tests", "prim_tests", "hits", "sky_lookups", "segments", "wave_node_iters", "wave_prim_iters",
              "wave_hits", "wave_sky", "leaf_rounds", "family_execs", "family_execs_compacted", "leaf_round_lanes",
-             "leaf_pairs", "family_execs_compacted_in_round")
+             "leaf_pairs", "family_execs_compacted_in_round", "repairs")
 
 
 def lane_utilisation(st):
@@ -400,6 +430,10 @@ def record(cfg, run, elapsed, kernel_ms, steps, st, n, with_profile=True):
             "lds_l2_effective_GBs": round(alg / avg_launch_s / 1e9, 1),
             "bytes_per_sample": round(alg / samples_launch, 1),
             "segments_per_sample": round(st["segments"] / max(st["samples"], 1), 3),
+            # leaf rounds whose sphere test raised t_max (Hittable.inl:152-158) and rebuilt the pending
+            # far children (repair_pending), in the default kernel's instrumented chunk
+            "rise_repairs_per_Msample": (round(st["d_repairs"] / max(st["samples"], 1) * 1e6, 3)
+                                         if "d_repairs" in st else None),
             "lane_utilisation": lane_utilisation(st)}
     if prof:
         c = prof["counters"]
@@ -510,6 +544,8 @@ def main():
                                      "synchronous launch each (libpt_host -> pt_render); gpu_ms_per_step = sum of "
                                      "getTiming() (the loop's totalGpuTime); fused_over_loop = loop step time / "
                                      "headline (one chunked launch) step time"})
+            if args.config == "C3" and args.cold:
+                recs.append(cold_one_shot(cfg, W, H, spp, local_rank, elapsed / args.steps, use_torch))
             for label in ("C2",) + tuple(x for x in args.extra.split(",") if x):
                 c2 = CONFIGS[label]
                 r2 = Run(c2, c2["width"], c2["height"], c2["spp"], 0, 1, local_rank, 1, "single")

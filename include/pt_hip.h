@@ -107,6 +107,10 @@ typedef struct pt_render_stats {
     uint64_t leaf_round_lanes;
     uint64_t leaf_pairs;
     uint64_t family_execs_compacted_in_round;
+    /* child-box walks: leaf rounds that ended with t_max above its value at the leaf's start (the
+     * sphere's far-root quirk, Hittable.inl:152-158) and rebuilt the reference's pending far
+     * children (trace.cu:48-98; repair_pending in pt_kernels.hip) */
+    uint64_t repairs;
 } pt_render_stats;
 
 typedef struct pt_context pt_context;
@@ -243,6 +247,11 @@ PT_API int pt_set_issue_priority(pt_context *ctx, int mode, uint32_t level3, uin
  * 0 = automatic (K = 4 at <= 2 samples per pixel on large images), 1 = off, K = 2..16 = always K
  * (resumable variants).  Results are identical for every setting. */
 PT_API int pt_set_strip_units(pt_context *ctx, int mode);
+/* Test knob (negative control): enabled = 0 skips the child-box walks' rebuild of the pending far
+ * children after a leaf raised t_max (the sphere's far-root quirk, Hittable.inl:152-158), so those
+ * walks drop boxes the reference would test (trace.cu:48-98) and results are NOT the reference's on
+ * rays that meet the quirk.  Default 1.  Exists so a test can show that a scene exercises the rebuild. */
+PT_API int pt_set_rise_repair(pt_context *ctx, int enabled);
 PT_API int pt_set_sample_groups(pt_context *ctx, int mode);
 PT_API int pt_set_patch_rounds(pt_context *ctx, uint32_t rounds);
 PT_API int pt_set_group_lookback(pt_context *ctx, uint32_t far, uint32_t near);

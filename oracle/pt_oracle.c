@@ -998,6 +998,8 @@ typedef struct {
 
 typedef struct {               /* counters for SURVEY.md §8(d) algorithmic bytes */
     uint64_t node_tests, prim_tests, hits, sky_lookups, segments, samples, max_stack;
+    uint64_t rises;            /* leaf visits that end with t_max above its value at the leaf's start
+                                  (hit_sphere's far root t1 > t_max, Hittable.inl:152-158) */
 } or_stats;
 
 /* hitBVH (trace.cu:28-98) */
@@ -1018,6 +1020,7 @@ static int hit_bvh(const or_scene *s, const ray_t *r, float tMin, float tMax, hi
         if (aabb_hit(node->bmin, node->bmax, r, tMin, tMax)) {
             const uint32_t cnt = node->primitiveCountAxis >> 16;
             if (cnt > 0) {
+                const float tLeaf = tMax;
                 for (uint32_t i = 0; i < cnt; ++i) {
                     if (st) st->prim_tests++;
                     if (hittable_hit(&s->prims[node->offset + i], r, tMin, tMax, rec)) {
@@ -1025,6 +1028,7 @@ static int hit_bvh(const or_scene *s, const ray_t *r, float tMin, float tMax, hi
                         elem = node->offset + i;
                     }
                 }
+                if (st && tMax > tLeaf) st->rises++;
                 if (sp == 0) break;
                 cur = stack[--sp];
             } else {
@@ -1389,13 +1393,14 @@ OR_EXPORT int or_render(const or_hittable *prims, uint32_t primCount, const or_b
         else render_rows(j);
     }
     int err = 0;
-    uint64_t agg[7] = { 0 };
+    uint64_t agg[8] = { 0 };
     for (int t = 0; t < nthreads; ++t) {
         if (nthreads > 1) pthread_join(th[t], NULL);
         err |= jobs[t].err;
         agg[0] += jobs[t].stats.node_tests; agg[1] += jobs[t].stats.prim_tests; agg[2] += jobs[t].stats.hits;
         agg[3] += jobs[t].stats.sky_lookups; agg[4] += jobs[t].stats.segments; agg[5] += jobs[t].stats.samples;
         if (jobs[t].stats.max_stack > agg[6]) agg[6] = jobs[t].stats.max_stack;
+        agg[7] += jobs[t].stats.rises;
     }
     if (stats_out) memcpy(stats_out, agg, sizeof(agg));
     free(jobs);

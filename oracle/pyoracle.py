@@ -383,14 +383,14 @@ class OracleRenderer:
         lib().or_init_rand_state(width, height, band_rows, row_offset, row_stride, self.rng)
         self.frames = 0
         self.threads = threads or default_threads()
-        self.stats = np.zeros(7, dtype=np.uint64)
+        self.stats = np.zeros(8, dtype=np.uint64)   # node, prim tests, hits, sky, segments, samples, max stack, rises
         self.fast = fast
 
     def render(self, camera: Camera, spp: int, ignore_history: bool, chunks: int = 1, collect_stats: bool = False) -> None:
         """`chunks` successive reference render(camera, spp, ignore_history and c == 0) calls."""
         sc = self.scene
         tex = sc.texture_table()
-        st = (C.c_uint64 * 7)() if collect_stats else None
+        st = (C.c_uint64 * 8)() if collect_stats else None
         rc = lib(self.fast).or_render(sc.prims, sc.prim_count, sc.nodes, sc.node_count, C.byref(camera), sc.skybox, tex,
                              len(sc.textures), self.width, self.height, self.band_rows, self.row_offset, self.row_stride,
                              fptr(self.accum), self.rng, spp, chunks, int(bool(ignore_history)), self.threads, st)

@@ -322,6 +322,12 @@ class Pathtracer:
         for c in self._contexts():
             N.check_ctx(N.hip().pt_set_strip_units(c, int(mode)), c)
 
+    def set_rise_repair(self, enabled: bool) -> None:
+        """Test knob (pt_set_rise_repair): False skips the rebuild of the pending far children after a
+        leaf raised t_max, so results are NOT the reference's on such rays (negative control)."""
+        for c in self._contexts():
+            N.check_ctx(N.hip().pt_set_rise_repair(c, int(bool(enabled))), c)
+
     def set_sample_groups(self, mode: int) -> None:
         """Speculative sample groups (pt_set_sample_groups): 0 = automatic, 1 = off, G >= 2 = always G."""
         for c in self._contexts():

@@ -45,7 +45,7 @@ class PtRenderStats(C.Structure):
                 ("cycles_leaf_tests", C.c_uint64), ("cycles_shading", C.c_uint64), ("cycles_total", C.c_uint64),
                 ("cycles_lane_idle", C.c_uint64), ("leaf_rounds", C.c_uint64), ("family_execs", C.c_uint64),
                 ("family_execs_compacted", C.c_uint64), ("leaf_round_lanes", C.c_uint64), ("leaf_pairs", C.c_uint64),
-                ("family_execs_compacted_in_round", C.c_uint64)]
+                ("family_execs_compacted_in_round", C.c_uint64), ("repairs", C.c_uint64)]
 
 
 # symbol -> (restype, argtypes); the CPU test suite checks that every declaration in include/*.h
@@ -73,6 +73,7 @@ _HIP_SYMBOLS = {
     "pt_read_tile_costs": (C.c_int, [C.c_void_p, P(C.c_uint32), C.c_uint32]),
     "pt_read_tile_idle": (C.c_int, [C.c_void_p, P(C.c_uint32), C.c_uint32]),
     "pt_set_strip_units": (C.c_int, [C.c_void_p, C.c_int]),
+    "pt_set_rise_repair": (C.c_int, [C.c_void_p, C.c_int]),
     "pt_unpermute_bands": (C.c_int, [C.c_int, C.c_void_p, C.c_void_p, C.c_uint32, C.c_uint32, C.c_uint32, C.c_uint32,
                                      C.c_uint32]),
     "pt_set_kernel_variant": (C.c_int, [C.c_void_p, C.c_int]),

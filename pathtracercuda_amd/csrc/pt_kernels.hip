@@ -124,7 +124,7 @@ static inline uint32_t ssg_window_words(uint32_t G, uint32_t n)
     return G == 2 ? (n * 6u + 256u + 63u) / 64u : kWinWords;
 }
 constexpr uint32_t kFoldBatch = 16;       // samples the fold loads at once
-constexpr uint32_t kStatWords = 22;       // counters of an instrumented launch (pt_render_stats)
+constexpr uint32_t kStatWords = 23;       // counters of an instrumented launch (pt_render_stats)
 constexpr uint32_t kStartWords = 8;       // start record: offset, d, v0..v4, stop offset (last group)
 enum : uint32_t { F_ACC = 0, F_COL = 3, F_SC = 6, F_DONE = 7, F_OFF = 8, F_H = 9, F_ST = 10, F_FLAG = 16, F_ODD = 17,
                   F_SQ = 18, kFoldWords = 19 };
@@ -314,6 +314,7 @@ struct Counters {
     uint64_t cyc_lane_idle;     // per lane: cycles between finishing its pixel and the tile's end
     uint32_t w_leaf_rounds, w_fam_exec, w_fam_ideal;   // leaf tests by shape family (pt_render_stats)
     uint32_t w_leaf_lanes, w_leaf_pairs, w_fam_inplace;  // lanes and (lane, primitive) pairs per leaf round
+    uint32_t repairs;           // leaf rounds that raised t_max and rebuilt the pending set (repair_pending)
 };
 
 // Shape family of a primitive test's code path in prim_hit: 0 plane (disk, quad), 1 cube, 2 quadric.
@@ -762,8 +763,10 @@ PT_DEV uint32_t traverse_cb(const float4* __restrict__ cnodes, const float4* __r
         // dropped for failing an earlier, smaller t_max may pass now.  (A rise undone within the leaf
         // needs nothing: every dropped box failed a t_max at least as large as the one left.)
         const bool rose = tMax > tLeaf;
-        if (__ballot(rose) != 0ull && rose)                    // rare: a uniform test first
+        if (__ballot(rose) != 0ull && rose) {                  // rare: a uniform test first
             repair_pending(cnodes, stack, R, negMask, tMin, P.rootWord, leaf0, sp);
+            if (STATS) cnt.repairs++;
+        }
         if (STATS) wave_time(cnt.cyc_leaf, tPhase);
         if (!pop()) done = true;
     }
@@ -785,8 +788,9 @@ struct TravState {
 };
 
 // The interior walk is walk_interior (the lean form: wave-uniform slab-form choice, unconditional
-// far-child write).  WW = 200 + EXITQ selects this traversal.
-template <bool STATS, int EXITQ>
+// far-child write).  WW = 200 + EXITQ selects this traversal.  NOREPAIR (a test-only instantiation,
+// pt_set_rise_repair) skips repair_pending: the negative control that shows a scene exercises it.
+template <bool STATS, int EXITQ, bool NOREPAIR = false>
 PT_DEV bool traverse_cb_phase(const float4* __restrict__ cnodes, const float4* __restrict__ prims, uint2* stack,
                               const TraceParams& P, f3 o, f3 d, bool fresh, TravState& ts, Counters& cnt)
 {
@@ -851,8 +855,10 @@ PT_DEV bool traverse_cb_phase(const float4* __restrict__ cnodes, const float4* _
         // dropped for failing an earlier, smaller t_max may pass now.  (A rise undone within the leaf
         // needs nothing: every dropped box failed a t_max at least as large as the one left.)
         const bool rose = tMax > tLeaf;
-        if (__ballot(rose) != 0ull && rose)                    // rare: a uniform test first
+        if (!NOREPAIR && __ballot(rose) != 0ull && rose) {     // rare: a uniform test first
             repair_pending(cnodes, stack, R, negMask, tMin, P.rootWord, leaf0, sp);
+            if (STATS) cnt.repairs++;
+        }
         if (STATS) wave_time(cnt.cyc_leaf, tPhase);
         if (!pop()) { done = true; break; }
         // early exit once at most EXITQ/64 of the lanes that entered are still walking
@@ -1176,6 +1182,7 @@ PT_DEV void flush_counters(const TraceParams& P, const Counters& cnt)
     atomicAdd(&P.stats[19], (unsigned long long)cnt.w_leaf_lanes);
     atomicAdd(&P.stats[20], (unsigned long long)cnt.w_leaf_pairs);
     atomicAdd(&P.stats[21], (unsigned long long)cnt.w_fam_inplace);
+    atomicAdd(&P.stats[22], (unsigned long long)cnt.repairs);
 }
 
 // One atomic per wave: the first active lane adds n to *cursor; the old value is read back from
@@ -1545,6 +1552,7 @@ __global__ void __launch_bounds__(WPB * 64, MINW) trace_kernel(TraceParams P)
             // SKYQ (WW / 10000): the same for misses (sky lookup, end of path, next camera ray).
             // DEFERQ + SKYQ <= 8, so when every live lane is ready one class always runs.
             constexpr int DEFERQ = (WW / 1000) % 10, SKYQ = (WW / 10000) % 10;
+            constexpr bool NOREPAIR = (WW / 100000) % 10 != 0;     // test-only (pt_set_rise_repair)
             static_assert(DEFERQ + SKYQ <= 8, "a wave whose lanes are all ready must shade one class");
             bool fresh = true, held = false;
             TravState ts = {0u, 0u, 0xffffffffu, kFltMax};
@@ -1552,7 +1560,7 @@ __global__ void __launch_bounds__(WPB * 64, MINW) trace_kernel(TraceParams P)
                 if (STATS && fresh && !held) { cnt.segments++; wave_tick(cnt.w_segments); }
                 bool tdone = true;
                 if (!held) {
-                    tdone = traverse_cb_phase<STATS, WW % 100>(nodes, prims, reinterpret_cast<uint2*>(stack), P,
+                    tdone = traverse_cb_phase<STATS, WW % 100, NOREPAIR>(nodes, prims, reinterpret_cast<uint2*>(stack), P,
                                                                 ps.o, ps.d, fresh, ts, cnt);
                     fresh = tdone;
                 }
@@ -2038,6 +2046,7 @@ struct pt_context {
     float4* cnodes = nullptr;   // child-box records (traverse_cb); null when the scene exceeds its encoding
     uint32_t cnodeCount = 0, rootWord = 0;
     bool dfsOrder = true;             // leaves hold their primitives in DFS order (repair_pending)
+    bool riseRepair = true;           // pt_set_rise_repair (tests' negative control only)
     float rootBox[6] = {};
     uint32_t nodeCount = 0, primCount = 0, stackDepth = 1;
     bool slabFast = true;
@@ -2130,7 +2139,10 @@ static hipError_t launch_one(const TraceParams& P, hipStream_t stream)
     const size_t nodeF4 = WW >= 3 ? 4 * (size_t)P.cnodeCount : 2 * (size_t)P.nodeCount;
     const size_t sceneBytes = ((SL >= 1 ? nodeF4 : 0) + (SL >= 2 ? 4 * (size_t)P.primCount : 0)) * sizeof(float4);
     const size_t lds = sceneBytes + (size_t)WPB * P.stackDepth * 64 * (WW >= 3 ? 8 : 4) + (size_t)WPB * 64 * 12;
-    if (WW >= 3 && P.cnodes == nullptr) return MODE == 1 ? hipErrorInvalidValue : launch_one<STATS, SL, WPB, 1, MINW, PERSIST, MODE>(P, stream);  // no child-box layout
+    // no child-box layout: the node-at-a-time walk -- except for grouped and strip launches, whose
+    // item and strip hand-off logic lives only in the resumable walk (pick_variant never sends them here)
+    if (WW >= 3 && P.cnodes == nullptr)
+        return (MODE == 1 || MODE == 3) ? hipErrorInvalidValue : launch_one<STATS, SL, WPB, 1, MINW, PERSIST, MODE>(P, stream);
     if (lds > 160 * 1024) {
         // scene too large to stage in LDS: the same variant reading the scene through the caches
         if (SL > 0) return launch_one<STATS, 0, WPB, WW, MINW, PERSIST, MODE>(P, stream);
@@ -2186,7 +2198,7 @@ static hipError_t launch_one(const TraceParams& P, hipStream_t stream)
 //   4   node-at-a-time while-while, caches, 5 waves/SIMD   (scenes outside the child-box encoding)
 //   6   node-at-a-time while-while, nodes in LDS           (idem, small BVH)
 //   20  child-box traversal, one tile per wave             (counts the reference's node/prim tests)
-// The WW parameter of the resumable walk encodes 10000 * SKYQ + 1000 * DEFERQ + 200 + EXITQ
+// The WW parameter of the resumable walk encodes 100000 * NOREPAIR + 10000 * SKYQ + 1000 * DEFERQ + 200 + EXITQ
 // (deferred shading and the traversal's exit threshold, see trace_kernel).
 //   39  variant 40 without deferred shading, exit <= 24/64 (the round-1 default; A/B reference)
 //   40  default: resumable lean child-box walk, records in LDS, persistent waves, deferred shading
@@ -2215,6 +2227,7 @@ static hipError_t launch_variant(int v, const TraceParams& P, hipStream_t stream
     case 46: return launch_one<STATS, 0, 4, 14212, 4, true, MODE>(P, stream);
     case 47: return launch_one<STATS, 1, 4, 224, 4, true, MODE>(P, stream);
     case 48: return launch_one<STATS, 2, 4, 13216, 4, true, MODE>(P, stream);
+    case 90: return launch_one<false, 1, 4, 100000 + kV40Walk, 5, true, 0>(P, stream);   // test only: 40, no repair
     default: return hipErrorInvalidValue;
     }
 }
@@ -2255,11 +2268,11 @@ static bool strip_capable(int v) { return v == 40 || v == 41 || v == 46; }
 // wave slot; the variant must be a strip-capable one.
 constexpr uint64_t kStripMaxSamples = 2;
 
+// `variant` is the one that runs (pick_variant's result, which already replaces a forced child-box
+// variant by a node-at-a-time one on scenes without the child-box layout or DFS leaf order).
 static uint32_t strip_tiles(const pt_context* ctx, int variant, uint32_t tiles, uint64_t samples)
 {
-    if (ctx->stripMode == 1) return 1;
-    const int v = ctx->variant ? ctx->variant : variant;
-    if (!strip_capable(v) && !(ctx->variant == 0 && (v == 40 || v == 41 || v == 46))) return 1;
+    if (ctx->stripMode == 1 || !strip_capable(variant) || !ctx->cnodes) return 1;
     if (ctx->stripMode >= 2) return (uint32_t)ctx->stripMode;
     if (samples > kStripMaxSamples) return 1;
     int cus = 0;
@@ -2282,9 +2295,11 @@ static int pick_variant(const pt_context* ctx)
 {
     const size_t nodeBytes = 2 * (size_t)ctx->nodeCount * sizeof(float4);
     if (ctx->variant > 0) {
-        // a child-box walk needs leaves in DFS primitive order for repair_pending (ChildPair)
+        // a child-box walk needs the child-box layout (leaf counts < 256) and leaves in DFS primitive
+        // order (repair_pending, ChildPair); without them the node-at-a-time walk runs, so grouped and
+        // strip launches (which exist only for the child-box walks) are never chosen for such scenes
         const bool childBox = ctx->variant != 1 && ctx->variant != 4 && ctx->variant != 6;
-        return (childBox && !ctx->dfsOrder) ? (nodeBytes <= 48 * 1024 ? 6 : 4) : ctx->variant;
+        return (childBox && (!ctx->dfsOrder || !ctx->cnodes)) ? (nodeBytes <= 48 * 1024 ? 6 : 4) : ctx->variant;
     }
     // measured on MI355X (tools/ab_variants.py, profiles/): child-box traversal (one dependent
     // fetch per interior visit, leaves inline) with while-while leaf batching and 5 waves/SIMD
@@ -2583,20 +2598,24 @@ PT_API int pt_set_scene(pt_context* ctx, const pt_bvh_node* nodes, uint32_t node
     // on the path to v -- their far child is pushed (and repair_pending rebuilds exactly these).
     // The walks write one entry unconditionally above the top at an interior visit (walk_interior;
     // the node-at-a-time walks push there), so the rows needed are the maximum over the 8 direction
-    // octants of pend(v) + 1 over interior v; pend(v) <= depth(v) - 1, the reference's bound.
+    // octants of pend(v) + 1 over interior v; pend(v) <= depth(v) - 1, the reference's bound.  pend is
+    // carried down the same root DFS validate_scene runs (only reachable nodes; an orphan node that
+    // names a reachable child cannot overwrite that child's value).
     {
-        std::vector<uint8_t> pend(node_count);
         uint32_t need = 1;
+        std::vector<std::pair<uint32_t, uint32_t>> st;
         for (uint32_t o = 0; o < 8; ++o) {
-            pend[0] = 0;
-            for (uint32_t i = 0; i < node_count; ++i) {
+            st.assign(1, {0u, 0u});
+            while (!st.empty()) {
+                const auto [i, pend] = st.back();
+                st.pop_back();
                 const uint32_t pca = nodes[i].primitive_count_axis;
                 if ((pca >> 16) != 0) continue;
+                need = std::max(need, pend + 1u);
                 const bool neg = (o >> ((pca >> 8) & 0xffu)) & 1u;
                 const uint32_t a = i + 1, b = nodes[i].offset;
-                pend[neg ? b : a] = (uint8_t)(pend[i] + 1);
-                pend[neg ? a : b] = pend[i];
-                need = std::max<uint32_t>(need, pend[i] + 1u);
+                st.push_back({neg ? b : a, pend + 1u});    // near child: its sibling is pending
+                st.push_back({neg ? a : b, pend});
             }
         }
         ctx->stackDepth = std::min(need, maxDepth > 1 ? maxDepth - 1 : 1u);
@@ -2955,7 +2974,8 @@ static int render_impl(pt_context* ctx, const pt_camera* cam, uint32_t spp, uint
     // Strip units (MODE 3, trace_kernel): launches of few samples per pixel dispatch row strips of K
     // tiles, and a lane whose pixel is done moves on to the next tile of its strip.  The cost order
     // is over units, so it is rebuilt when K changes.
-    const uint32_t K = (sorted && !stats) ? strip_tiles(ctx, pick_variant(ctx), tiles, (uint64_t)spp * chunks) : 1u;
+    const bool noRepair = !ctx->riseRepair;           // test knob: plain launches of variant 90 only
+    const uint32_t K = (sorted && !stats && !noRepair) ? strip_tiles(ctx, pick_variant(ctx), tiles, (uint64_t)spp * chunks) : 1u;
     const uint32_t unitsX = (P.tilesX + K - 1) / K, units = unitsX * P.tilesY;
     if (K != ctx->orderStrip) {
         ctx->orderValid = false;
@@ -3004,8 +3024,13 @@ static int render_impl(pt_context* ctx, const pt_camera* cam, uint32_t spp, uint
     const uint32_t total = spp * chunks;
     // the fold state packs (sample in call, call) into one word as sIdx | c << 16 (ssg_fold_kernel)
     const bool groupable = !stats && sorted && (uint64_t)spp * chunks < (1ull << 31) && spp <= 0xffffu && chunks <= 0xffffu;
-    uint32_t G = groupable && K == 1 ? ssg_groups(ctx, variant, tiles, total) : 0;
-    if (!G && ctx->variant == 0 && K == 1) variant = small_grid_variant(ctx, variant, tiles);
+    uint32_t G = groupable && K == 1 && !noRepair ? ssg_groups(ctx, variant, tiles, total) : 0;
+    if (!G && ctx->variant == 0 && K == 1 && !noRepair) variant = small_grid_variant(ctx, variant, tiles);
+    if (noRepair) {
+        if (variant != 40 || stats)
+            return fail(ctx, PT_ERR_STATE, "pt_set_rise_repair(0): only plain launches of variant 40 have a no-repair build");
+        variant = 90;
+    }
     // Grouped launches of at most one tile per wave slot (one rank's 1080p share at N = 8) are
     // short items whose latency sets the launch: deferred shading, which trades a lane's latency for
     // fuller hit-shading rounds, measured bimodal there (median 57.7-62.6 ms against 57.8-58.2 ms
@@ -3103,7 +3128,15 @@ static int render_impl(pt_context* ctx, const pt_camera* cam, uint32_t spp, uint
         stats->leaf_round_lanes = h[19];
         stats->leaf_pairs = h[20];
         stats->family_execs_compacted_in_round = h[21];
+        stats->repairs = h[22];
     }
+    return PT_OK;
+}
+
+PT_API int pt_set_rise_repair(pt_context* ctx, int enabled)
+{
+    if (!ctx || enabled < 0 || enabled > 1) return PT_ERR_ARG;
+    ctx->riseRepair = enabled != 0;
     return PT_OK;
 }
 

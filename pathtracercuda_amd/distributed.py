@@ -56,9 +56,14 @@ def gather_framebuffer(local, height: int, rank: int, world: int, recv=None, ful
         dist.gather(local, recv, dst=0)
         if full is None:
             full = torch.empty((height,) + tuple(local.shape[1:]), dtype=local.dtype, device=local.device)
-        if local.device.type == "cuda":
+        native = (local.device.type == "cuda" and local.dtype == torch.float32 and local.dim() == 3
+                  and int(local.shape[-1]) == 4 and full.dtype == torch.float32 and full.is_contiguous()
+                  and all(t.is_contiguous() and t.dtype == torch.float32 for t in recv))
+        if native:
             # on the GPU the scatter is the native unpermute kernel -- the same one pt_group_gather
-            # runs after its RCCL gather -- so both multi-GPU front ends assemble the image identically
+            # runs after its RCCL gather -- so both multi-GPU front ends assemble the image identically.
+            # It moves float4 rows, so only a contiguous (rows, W, 4) float32 framebuffer takes it;
+            # anything else takes the index copy below.
             from . import _native as N
             width = int(local.shape[1])
             for r in range(world):
@@ -67,7 +72,7 @@ def gather_framebuffer(local, height: int, rank: int, world: int, recv=None, ful
                 if rc != 0:
                     raise RuntimeError(f"pt_unpermute_bands failed ({rc})")
             return full
-        # CPU tensors (the gloo tests): the same row map (global_rows), as a torch index copy
+        # CPU tensors (the gloo tests) and other layouts: the same row map (global_rows), as a torch index copy
         for r in range(world):
             idx = index[r] if index is not None else torch.tensor(global_rows(height, r, world, band_rows),
                                                                   dtype=torch.long, device=local.device)

@@ -661,3 +661,109 @@ def test_rise_repair_matches_reference_rule(gpu_available, scenes, scene, W, H, 
         out.append(pt.accum().view(np.uint32).copy())
     diff = int((out[0] != out[1]).any(-1).sum())
     assert diff == 0, f"{scene}: {diff} pixels differ from the reference's control flow"
+
+
+def test_rise_repair_runs_and_is_exact_vs_oracle(gpu_available, scenes):
+    # VERDICT r04 "do this" 1.  scenes/rise_repair.scene.json (tools/make_test_fixtures.py) puts the
+    # camera and every object inside one large sphere: leaves whose sphere test takes the far root
+    # (Hittable.inl:152-158) raise t_max in mid traversal on about a third of the samples, and the
+    # reference then tests the boxes it pops at the larger t_max (trace.cu:48-98).
+    #  1. the default launch is bit-exact against the ORACLE (not only against variant 1);
+    #  2. the instrumented launch's repairs counter (leaf rounds that rebuilt the pending set) is
+    #     positive and equals the oracle's count of leaf visits that raised t_max -- the two walks
+    #     visit the same leaves in the same order;
+    #  3. negative control: the same launch without the rebuild (variant 40 compiled without it,
+    #     pt_set_rise_repair(0)) is NOT the oracle's, so the scene really needs the repair.
+    W, H, spp, chunks = 96, 64, 4, 2
+    pt, cam, ref, osc = pair(scenes / "rise_repair.scene.json", W, H)
+    st = pt.rng_state()
+    ref.render(osc.camera, spp, True, chunks=chunks, collect_stats=True)
+    rises = int(ref.stats[7])
+    assert rises > 0
+    for variant in (0, 40, 20):
+        pt.set_kernel_variant(variant)
+        pt.set_rng_state(st)
+        pt.render_raw(cam, spp, chunks, True)
+        assert_bitexact(pt.accum(), ref.accum, f"rise scene, variant {variant}")
+        assert np.array_equal(pt.rng_state(), ref.rng_array()), f"rise scene, variant {variant}: RNG"
+    for variant in (40, 20):
+        pt.set_kernel_variant(variant)
+        pt.set_rng_state(st)
+        stats = pt.render_instrumented(cam, spp, chunks, True)
+        assert stats["repairs"] == rises, (variant, stats["repairs"], rises)
+        assert_bitexact(pt.accum(), ref.accum, f"rise scene, instrumented variant {variant}")
+    pt.set_kernel_variant(40)
+    pt.set_rise_repair(False)
+    pt.set_rng_state(st)
+    pt.render_raw(cam, spp, chunks, True)
+    got = pt.accum()
+    pt.set_rise_repair(True)
+    differ = int((bits(got) != bits(ref.accum)).any(-1).sum())
+    assert differ > 0.01 * W * H, f"negative control: only {differ} pixels differ without the repair"
+
+
+def _set_caller_bvh(pt, osc, nodes):
+    """Hand a caller BVH (tests/bvh_edit.py node tuples) to pt_set_scene with the scene's primitives."""
+    import ctypes as C
+    from pathtracercuda_amd import _native as N
+    arr = (pa.PtBvhNode * len(nodes))()
+    for i, (lo, hi, off, pca) in enumerate(nodes):
+        arr[i].aabb_min[:] = list(lo)
+        arr[i].aabb_max[:] = list(hi)
+        arr[i].offset = off
+        arr[i].primitive_count_axis = pca
+    prims = (pa.PtHittable * osc.prim_count).from_buffer_copy(bytes(osc.prims)[:osc.prim_count * C.sizeof(pa.PtHittable)])
+    N.check_ctx(N.hip().pt_set_scene(pt._ctx, arr, len(nodes), prims, osc.prim_count), pt._ctx)
+
+
+def test_orphan_node_bvh_renders_exactly(gpu_available, scenes):
+    # ADVICE r04: a caller BVH with an unreachable interior node that names a deep reachable node as
+    # its child.  The stack-row bound is now taken over the tree reachable from the root (the
+    # array-order form gave 16 rows instead of 29 here, tests/test_bvh_validation.py), so the walks
+    # stay inside their LDS rows; the render equals the oracle's on the same tree without the orphan.
+    from test_bvh_validation import orphan_caterpillar
+    W, H = 96, 64
+    pt, cam, ref, osc = pair(scenes / "generated_scene.scene.json", W, H)
+    cat, bad = orphan_caterpillar(osc)
+    ref_nodes = (po.BVHNode * len(cat))()
+    for i, (lo, hi, off, pca) in enumerate(cat):
+        ref_nodes[i].bmin[:] = list(lo)
+        ref_nodes[i].bmax[:] = list(hi)
+        ref_nodes[i].offset = off
+        ref_nodes[i].primitiveCountAxis = pca
+    osc.nodes = ref_nodes
+    osc.node_count = len(cat)
+    ref.render(osc.camera, 4, True, chunks=2)
+    _set_caller_bvh(pt, osc, bad)
+    st = pt.rng_state()
+    for variant in (0, 40, 41, 39, 20):
+        pt.set_kernel_variant(variant)
+        pt.set_rng_state(st)
+        pt.render_raw(cam, 4, 2, True)
+        assert_bitexact(pt.accum(), ref.accum, f"orphan BVH, variant {variant}")
+
+
+def test_forced_strip_variant_without_child_box_layout(gpu_available, scenes):
+    # ADVICE r04: a forced child-box variant with strip units on a scene outside the child-box
+    # encoding (one leaf of 484 > 255 primitives) runs the node-at-a-time walk, unit-less: every tile
+    # rendered, the oracle's bits (before round 5 only the first tile of each strip was rendered)
+    import ctypes as C
+    from pathtracercuda_amd import _native as N
+    W, H = 256, 96
+    pt, cam, ref, osc = pair(scenes / "generated_scene.scene.json", W, H)
+    root = po.BVHNode.from_buffer_copy(bytes(osc.nodes[0]))
+    root.offset = 0
+    root.primitiveCountAxis = osc.prim_count << 16
+    osc.nodes = (po.BVHNode * 1)(root)
+    osc.node_count = 1
+    nodes = (pa.PtBvhNode * 1).from_buffer_copy(bytes(osc.nodes))
+    prims = (pa.PtHittable * osc.prim_count).from_buffer_copy(bytes(osc.prims)[:osc.prim_count * C.sizeof(pa.PtHittable)])
+    N.check_ctx(N.hip().pt_set_scene(pt._ctx, nodes, 1, prims, osc.prim_count), pt._ctx)
+    ref.render(osc.camera, 1, True, chunks=2)
+    st = pt.rng_state()
+    for variant in (40, 41, 46):
+        pt.set_kernel_variant(variant)
+        pt.set_strip_units(4)
+        pt.set_rng_state(st)
+        pt.render_raw(cam, 1, 2, True)
+        assert_bitexact(pt.accum(), ref.accum, f"no child-box layout, forced variant {variant}, strip 4")

@@ -179,3 +179,21 @@ def test_fast_timing_build_is_bit_identical(scenes):
     b.render(sc.camera, 4, True, chunks=2)
     assert np.array_equal(a.accum.view(np.uint32), b.accum.view(np.uint32))
     assert np.array_equal(a.rng_array(), b.rng_array())
+
+
+def test_rise_scene_exercises_the_far_root_quirk(scenes):
+    # scenes/rise_repair.scene.json puts the camera and every object inside one large sphere, so the
+    # reference's hitBVH (trace.cu:48-98) meets leaves whose sphere test returns the far root beyond
+    # t_max (Hittable.inl:152-158) and raises t_max mid-traversal.  The oracle counts such leaf visits
+    # ("rises"); the GPU parity test asserts its repairs counter equals this count.  The shipped
+    # scenes meet the case rarely (generated_scene) or never at this size.
+    W, H = 48, 32
+    osc = po.load_scene(scenes / "rise_repair.scene.json", W, H)
+    r = po.OracleRenderer(osc, W, H)
+    r.render(osc.camera, 4, True, collect_stats=True)
+    rises = int(r.stats[7])
+    assert rises > 0.05 * int(r.stats[5]), f"rise scene: only {rises} rises in {int(r.stats[5])} samples"
+    osc = po.load_scene(scenes / "cornell_box.scene.json", W, H)
+    r = po.OracleRenderer(osc, W, H)
+    r.render(osc.camera, 4, True, collect_stats=True)
+    assert int(r.stats[7]) < rises

@@ -37,7 +37,7 @@ for step in "$@"; do
       rc=$?; tail -c 400 "$O/bench.json"; echo; fatal $rc bench;;
     kprof)
       echo "== rocprofv3 kernel trace"
-      (cd /tmp && timeout -k 10 600 rocprofv3 --kernel-trace --stats -d "$O/prof_bench" -o run --output-format csv -- python3 "$R/bench.py" --cpu-baseline 0 --call-loop 0 --extra '') > "$O/prof_bench.log" 2>&1
+      (cd /tmp && timeout -k 10 600 rocprofv3 --kernel-trace --stats -d "$O/prof_bench" -o run --output-format csv -- python3 "$R/bench.py" --cpu-baseline 0 --call-loop 0 --cold 0 --extra '') > "$O/prof_bench.log" 2>&1
       rc=$?; tail -1 "$O/prof_bench.log"; fatal $rc rocprof;;
     pmc)
       i=0

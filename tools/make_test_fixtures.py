@@ -3,7 +3,13 @@
                                  sphere / cylinder, an emissive light, metals, roughness extremes,
                                  a JSON-integer roughness (ignored by the loader, SceneLoader.cpp:165),
                                  an unknown material string, skybox lighting;
-  scenes/checker.png             64x32 RGB texture standing in for the reference's missing earth.png.
+  scenes/checker.png             64x32 RGB texture standing in for the reference's missing earth.png;
+  scenes/rise_repair.scene.json  the camera and every object inside one large emissive sphere, with
+                                 overlapping spheres and boxes: nearly every ray starts inside a
+                                 sphere, so the sphere test's far-root quirk (Hittable.inl:152-158,
+                                 t1 accepted beyond t_max when t0 <= t_min) raises t_max in mid
+                                 traversal and the reference then tests popped boxes at the larger
+                                 value (trace.cu:48-98) -- the case repair_pending exists for.
 """
 import json
 import pathlib
@@ -69,10 +75,34 @@ def scene() -> dict:
             "skybox": "skybox.hdr", "objects": objs}
 
 
+def rise_scene() -> dict:
+    objs = [obj("SPHERE", (0.0, 1.0, 0.0), (0.0, 0.0, 0.0), (6.0, 6.0, 6.0), "LAMBERT", (0.7, 0.7, 0.8),
+                emissive=(0.6, 0.6, 0.7)),
+            obj("QUAD", (0.0, 0.0, 0.0), (0.0, 0.0, 0.0), (3.0, 3.0, 3.0), "LAMBERT", (0.8, 0.8, 0.8))]
+    for i in range(4):
+        for j in range(3):
+            x = -1.8 + 1.2 * i
+            z = -1.5 + 1.2 * j
+            r = 0.25 + 0.05 * ((i + j) % 3)
+            m = MATS[(i + 2 * j) % 3]
+            base = (0.3 + 0.15 * i, 0.8 - 0.2 * j, 0.4 + 0.1 * (i + j) % 0.5)
+            shape = "SPHERE" if (i + j) % 2 == 0 else "CUBE"
+            objs.append(obj(shape, (x, r + 0.05 * j, z), (0.0, 20.0 * i, 10.0 * j), (r, r, r), m, base,
+                            rough=[0.1, 0.4, 0.8][j], metal=float((i + j) % 2)))
+    # overlapping pairs: a sphere cut by a box and a sphere around a smaller one (rays start inside)
+    objs.append(obj("SPHERE", (0.6, 0.9, 1.4), (0.0, 0.0, 0.0), (0.6, 0.6, 0.6), "GGX", (0.9, 0.9, 0.9), rough=0.3, metal=1.0))
+    objs.append(obj("CUBE", (0.9, 0.7, 1.6), (0.0, 35.0, 0.0), (0.35, 0.35, 0.35), "LAMBERT", (0.9, 0.3, 0.2)))
+    objs.append(obj("SPHERE", (-0.9, 1.2, 0.8), (0.0, 0.0, 0.0), (0.9, 0.9, 0.9), "LAMBERT_GGX", (0.4, 0.6, 0.9), rough=0.2))
+    objs.append(obj("SPHERE", (-0.9, 1.2, 0.8), (0.0, 0.0, 0.0), (0.3, 0.3, 0.3), "LAMBERT", (1.0, 1.0, 1.0), emissive=(4.0, 3.0, 2.0)))
+    objs.append(obj("CYLINDER", (1.8, 0.8, -0.4), (0.0, 0.0, 0.0), (0.3, 0.8, 0.3), "LAMBERT", (0.5, 0.9, 0.5)))
+    return {"camera": {"position": [0.0, 1.3, 4.0], "look_at": [0.0, 0.6, 0.0], "fovy": 50.0}, "objects": objs}
+
+
 def main() -> int:
     checker_png(ROOT / "scenes" / "checker.png")
     (ROOT / "scenes" / "test_shapes.scene.json").write_text(json.dumps(scene(), indent=1) + "\n")
-    print("wrote scenes/checker.png, scenes/test_shapes.scene.json")
+    (ROOT / "scenes" / "rise_repair.scene.json").write_text(json.dumps(rise_scene(), indent=1) + "\n")
+    print("wrote scenes/checker.png, scenes/test_shapes.scene.json, scenes/rise_repair.scene.json")
     return 0
 
 
