@@ -316,7 +316,7 @@ class CallLoopRun(Run):
         return total
 
 
-def cold_one_shot(cfg, W, H, spp, local_rank, warm_step_s, use_torch, reps=3):
+def cold_one_shot(cfg, W, H, spp, local_rank, use_torch, warm_step_s, reps=3):
     """A one-shot render the way `pathtracer -w W -h H -spp SPP` runs it (main.cpp:262-295): a fresh
     context (Pathtracer ctor, scene load: untimed), then ONE render of the whole workload with no tile
     costs yet -- the built-in cost pre-pass, its sort and the launch in the pre-pass's order, all
@@ -545,7 +545,7 @@ def main():
                                      "getTiming() (the loop's totalGpuTime); fused_over_loop = loop step time / "
                                      "headline (one chunked launch) step time"})
             if args.config == "C3" and args.cold:
-                recs.append(cold_one_shot(cfg, W, H, spp, local_rank, elapsed / args.steps, use_torch))
+                recs.append(cold_one_shot(cfg, W, H, spp, local_rank, use_torch, elapsed / args.steps))
             for label in ("C2",) + tuple(x for x in args.extra.split(",") if x):
                 c2 = CONFIGS[label]
                 r2 = Run(c2, c2["width"], c2["height"], c2["spp"], 0, 1, local_rank, 1, "single")
