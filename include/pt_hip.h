@@ -252,6 +252,15 @@ PT_API int pt_set_strip_units(pt_context *ctx, int mode);
  * walks drop boxes the reference would test (trace.cu:48-98) and results are NOT the reference's on
  * rays that meet the quirk.  Default 1.  Exists so a test can show that a scene exercises the rebuild. */
 PT_API int pt_set_rise_repair(pt_context *ctx, int enabled);
+/* Run-ahead across render() calls: a launch of 3..64 samples per pixel (the reference's
+ * render(camera, 8, ...) calls, main.cpp:272-279) lets the lanes whose pixels are done go on with the
+ * pixel's next call (same XORWOW stream) until their tile ends, and keeps those samples' colour sum,
+ * count and state per pixel; the next pt_render with the same camera, scene, textures, sky and RNG
+ * state starts every pixel from there.  Any other next launch ignores the stash: the stored RNG
+ * state and accumulation are always those of the calls made, so results are the reference's either
+ * way.  0 = automatic (the default; stops while the camera or scene changes at every launch),
+ * 1 = off, 2 = make a stash at every launch (tests). */
+PT_API int pt_set_run_ahead(pt_context *ctx, int mode);
 PT_API int pt_set_sample_groups(pt_context *ctx, int mode);
 PT_API int pt_set_patch_rounds(pt_context *ctx, uint32_t rounds);
 PT_API int pt_set_group_lookback(pt_context *ctx, uint32_t far, uint32_t near);

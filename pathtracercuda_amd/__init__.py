@@ -322,6 +322,12 @@ class Pathtracer:
         for c in self._contexts():
             N.check_ctx(N.hip().pt_set_strip_units(c, int(mode)), c)
 
+    def set_run_ahead(self, mode: int) -> None:
+        """Run-ahead across render() calls (pt_set_run_ahead): 0 automatic, 1 off, 2 always make a
+        stash.  Results are the reference's for every setting."""
+        for c in self._contexts():
+            N.check_ctx(N.hip().pt_set_run_ahead(c, int(mode)), c)
+
     def set_rise_repair(self, enabled: bool) -> None:
         """Test knob (pt_set_rise_repair): False skips the rebuild of the pending far children after a
         leaf raised t_max, so results are NOT the reference's on such rays (negative control)."""

@@ -74,6 +74,7 @@ _HIP_SYMBOLS = {
     "pt_read_tile_idle": (C.c_int, [C.c_void_p, P(C.c_uint32), C.c_uint32]),
     "pt_set_strip_units": (C.c_int, [C.c_void_p, C.c_int]),
     "pt_set_rise_repair": (C.c_int, [C.c_void_p, C.c_int]),
+    "pt_set_run_ahead": (C.c_int, [C.c_void_p, C.c_int]),
     "pt_unpermute_bands": (C.c_int, [C.c_int, C.c_void_p, C.c_void_p, C.c_uint32, C.c_uint32, C.c_uint32, C.c_uint32,
                                      C.c_uint32]),
     "pt_set_kernel_variant": (C.c_int, [C.c_void_p, C.c_int]),

@@ -111,6 +111,12 @@ struct TraceParams {
     uint32_t occCap;            // host only: persistent grids hold at most this many workgroups per CU (0 = all)
     uint32_t prio[3];           // issue priority by order position: < prio[0] -> 3, < prio[1] -> 2, < prio[2] -> 1
     uint32_t strip;             // MODE 3: tiles per dispatch unit (a row strip of `strip` tiles; see trace_kernel)
+    // MODE 4 (run-ahead across render() calls, see trace_kernel): per-pixel stash of the NEXT call's
+    // first samples, kAheadWords planes of rows x width u32: colour sum (3 f32), samples k, XORWOW
+    // state after them (6).  k = 0: no stash.
+    uint32_t* ahead;
+    uint32_t aheadUse;          // != 0: the stash was made under this launch's camera and scene: consume it
+    uint32_t aheadMake;         // != 0: lanes whose pixel is done go on with the next call's samples
 };
 
 // Speculative sample groups: window of a group's start offset in which an earlier group's parse can
@@ -126,6 +132,7 @@ static inline uint32_t ssg_window_words(uint32_t G, uint32_t n)
 constexpr uint32_t kFoldBatch = 16;       // samples the fold loads at once
 constexpr uint32_t kStatWords = 23;       // counters of an instrumented launch (pt_render_stats)
 constexpr uint32_t kStartWords = 8;       // start record: offset, d, v0..v4, stop offset (last group)
+constexpr uint32_t kAheadWords = 10;      // run-ahead stash: colour sum x3, samples, XORWOW state x6
 enum : uint32_t { F_ACC = 0, F_COL = 3, F_SC = 6, F_DONE = 7, F_OFF = 8, F_H = 9, F_ST = 10, F_FLAG = 16, F_ODD = 17,
                   F_SQ = 18, kFoldWords = 19 };
 
@@ -1126,28 +1133,169 @@ PT_DEV bool shade(const TraceParams& P, const float4* __restrict__ prims, uint32
     return false;
 }
 
+struct PixelCtx {
+    bool valid;
+    uint32_t px, py;
+    size_t li, npix;
+};
+
+PT_DEV PixelCtx pixel_of(const TraceParams& P, uint32_t tile, uint32_t lane)
+{
+    PixelCtx pc;
+    pc.npix = (size_t)P.rows * P.width;
+    if (P.scatterWaves) {
+        // scattered mapping: lane k of wave w takes local pixel k * waves + w, so every wave holds
+        // pixels from the whole tile of rows and all waves cost about the same
+        const size_t li = (size_t)lane * P.scatterWaves + tile;
+        pc.valid = tile < P.scatterWaves && li < pc.npix;
+        pc.li = pc.valid ? li : 0;
+        const uint32_t ly = (uint32_t)(pc.li / P.width);
+        pc.px = (uint32_t)(pc.li - (size_t)ly * P.width);
+        pc.py = global_row(ly, P.rowOffset, P.rowStride, P.bandShift);
+        return pc;
+    }
+    const uint32_t tileX = tile & 0xffffu, tileY = tile >> 16;   // packed (order entries)
+    pc.px = tileX * 8u + (lane & 7u);
+    const uint32_t ly = tileY * 8u + (lane >> 3);
+    pc.valid = tileY < P.tilesY && pc.px < P.width && ly < P.rows;
+    pc.py = global_row(ly, P.rowOffset, P.rowStride, P.bandShift);
+    pc.li = (size_t)ly * P.width + pc.px;
+    return pc;
+}
+
+template <bool AUX, bool AHEAD = false>
+PT_DEV void load_pixel(const TraceParams& P, const PixelCtx& pc, Xorwow& rng, PathState& ps, uint32_t accL)
+{
+    // AUX: resume launches (see ssg_fold_kernel; pixels the fold finished are skipped by the caller)
+    rng.d = P.rng[pc.li];
+    rng.v0 = P.rng[pc.npix + pc.li];
+    rng.v1 = P.rng[2 * pc.npix + pc.li];
+    rng.v2 = P.rng[3 * pc.npix + pc.li];
+    rng.v3 = P.rng[4 * pc.npix + pc.li];
+    rng.v4 = P.rng[5 * pc.npix + pc.li];
+    ps.acc = accL;
+    if (!P.ignoreFirst || (AUX && P.fold)) {     // the first call of an ignoreHistory launch overwrites it
+        const float4 a = P.accum[pc.li];
+        float* l = lds_f() + accL;
+        l[0] = a.x;
+        l[64] = a.y;
+        l[128] = a.z;
+    }
+    ps.color = splat(0.0f);
+    ps.L = splat(0.0f);
+    ps.T = splat(1.0f);
+    ps.s = ps.c = ps.bounce = 0;
+    ps.alive = P.chunks > 0 && P.spp > 0;
+    if (AUX && P.fold) {                         // mid-launch state left by ssg_fold_kernel
+        const uint32_t* F = P.fold;
+        ps.color = mk(__uint_as_float(F[(F_COL + 0) * pc.npix + pc.li]), __uint_as_float(F[(F_COL + 1) * pc.npix + pc.li]),
+                      __uint_as_float(F[(F_COL + 2) * pc.npix + pc.li]));
+        const uint32_t sc = F[F_SC * pc.npix + pc.li];
+        ps.s = sc & 0xffffu;
+        ps.c = sc >> 16;
+        ps.alive = ps.c < P.chunks;
+    }
+    if (AHEAD && P.aheadUse) {
+        // the previous launch's stash of this call's first k samples (same camera and scene: the
+        // host checked the key); a stash longer than this call's spp cannot be split and is dropped
+        const uint32_t* A = P.ahead;
+        const size_t n = pc.npix, li = pc.li;
+        const uint32_t k = A[3 * n + li];
+        if (k != 0u && k <= P.spp) {
+            ps.color = mk(__uint_as_float(A[li]), __uint_as_float(A[n + li]), __uint_as_float(A[2 * n + li]));
+            ps.s = k;
+            rng.d = A[4 * n + li];
+            rng.v0 = A[5 * n + li];
+            rng.v1 = A[6 * n + li];
+            rng.v2 = A[7 * n + li];
+            rng.v3 = A[8 * n + li];
+            rng.v4 = A[9 * n + li];
+        }
+    }
+}
+
+PT_DEV void store_pixel(const TraceParams& P, const PixelCtx& pc, const Xorwow& rng, const PathState& ps)
+{
+    // The pixel index passes through an empty asm so the store addresses are recomputed here from
+    // one 32-bit register: otherwise the compiler reuses the seven 64-bit addresses of load_pixel and
+    // keeps them live (spilled) across the whole tile.  Contexts hold < 2^30 pixels (pt_create).
+    uint32_t li = (uint32_t)pc.li;
+    asm volatile("" : "+v"(li));
+    P.rng[li] = rng.d;
+    P.rng[pc.npix + li] = rng.v0;
+    P.rng[2 * pc.npix + li] = rng.v1;
+    P.rng[3 * pc.npix + li] = rng.v2;
+    P.rng[4 * pc.npix + li] = rng.v3;
+    P.rng[5 * pc.npix + li] = rng.v4;
+    const float* a = lds_f() + ps.acc;
+    P.accum[li] = make_float4(a[0], a[64], a[128], 1.0f);   // trace.cu:198, once per launch
+}
+
 // End of a path: sum it into the render() call's color; at the end of a call fold the call into
 // the accumulation value (trace.cu:193-198); start the next sample while any remain.  The running
 // accumulation value lives in the wave's LDS slice for the whole launch (loaded by load_pixel,
 // stored once by store_pixel), so a launch of many render() calls writes each pixel once instead of
 // once per call -- the fold and its order (color + accum) are unchanged.
-template <bool STATS>
-PT_DEV void finish_path(const TraceParams& P, PathState& ps, Xorwow& rng, float fx, float fy, Counters& cnt)
+// Run-ahead (MODE 4): the pixel's samples of the NEXT render() call, summed in sample order from 0
+// and the XORWOW state after them, so that call can start from there (load_pixel) -- its colour sum
+// continues in the same order, so the fold color + accum (trace.cu:196) sees the same value.
+PT_DEV void ahead_store(const TraceParams& P, const PixelCtx& pc, const f3& color, uint32_t k, const Xorwow& rng)
+{
+    uint32_t li = (uint32_t)pc.li;
+    asm volatile("" : "+v"(li));                 // addresses from one register (store_pixel)
+    uint32_t* A = P.ahead;
+    const size_t n = pc.npix;
+    A[li] = __float_as_uint(color.x);
+    A[n + li] = __float_as_uint(color.y);
+    A[2 * n + li] = __float_as_uint(color.z);
+    A[3 * n + li] = k;
+    A[4 * n + li] = rng.d;
+    A[5 * n + li] = rng.v0;
+    A[6 * n + li] = rng.v1;
+    A[7 * n + li] = rng.v2;
+    A[8 * n + li] = rng.v3;
+    A[9 * n + li] = rng.v4;
+}
+
+// The end of a render() call's samples (ps.s == spp): fold the call into the accumulation value
+// (trace.cu:193-198).  AHEAD: a lane already in run-ahead (ps.c == chunks) has done a whole next call:
+// it stashes it and stops; a lane finishing its last call stores its pixel now (the call's RNG state
+// and accumulation are final here) and, when the launch makes a stash, goes on with the next call.
+template <bool AHEAD>
+PT_DEV void end_call(const TraceParams& P, const PixelCtx& pc, PathState& ps, const Xorwow& rng)
+{
+    if (AHEAD && ps.c == P.chunks) {
+        ahead_store(P, pc, ps.color, ps.s, rng);
+        ps.alive = false;
+        return;
+    }
+    const bool ignore = (ps.c == 0) && P.ignoreFirst;
+    f3 acc = ps.color;
+    float* a = lds_f() + ps.acc;
+    if (!ignore) acc = add(ps.color, mk(a[0], a[64], a[128]));
+    a[0] = acc.x;
+    a[64] = acc.y;
+    a[128] = acc.z;
+    ps.color = splat(0.0f);
+    ps.s = 0;
+    if (++ps.c == P.chunks) {
+        ps.alive = false;
+        if (AHEAD) {
+            store_pixel(P, pc, rng, ps);
+            P.ahead[3 * pc.npix + (uint32_t)pc.li] = 0u;      // no stash unless a next-call sample ends
+            ps.alive = P.aheadMake != 0;
+        }
+    }
+}
+
+template <bool STATS, bool AHEAD = false>
+PT_DEV void finish_path(const TraceParams& P, PathState& ps, Xorwow& rng, float fx, float fy, Counters& cnt,
+                        const PixelCtx& pc)
 {
     ps.color = add(ps.color, ps.L);
     if (STATS) cnt.samples++;
-    if (++ps.s == P.spp) {
-        const bool ignore = (ps.c == 0) && P.ignoreFirst;
-        f3 acc = ps.color;
-        float* a = lds_f() + ps.acc;
-        if (!ignore) acc = add(ps.color, mk(a[0], a[64], a[128]));
-        a[0] = acc.x;
-        a[64] = acc.y;
-        a[128] = acc.z;
-        ps.color = splat(0.0f);
-        ps.s = 0;
-        if (++ps.c == P.chunks) ps.alive = false;
-    }
+    if (++ps.s == P.spp) end_call<AHEAD>(P, pc, ps, rng);
+    else if (AHEAD && ps.c == P.chunks) ahead_store(P, pc, ps.color, ps.s, rng);   // a next-call sample
     if (ps.alive) {
         camera_ray(P, fx, fy, rng, ps.o, ps.d);
         ps.L = splat(0.0f);
@@ -1391,87 +1539,6 @@ PT_DEV void ssg_finish(const TraceParams& P, PathState& ps, Xorwow& rng, float f
     ps.bounce = 0;
 }
 
-struct PixelCtx {
-    bool valid;
-    uint32_t px, py;
-    size_t li, npix;
-};
-
-PT_DEV PixelCtx pixel_of(const TraceParams& P, uint32_t tile, uint32_t lane)
-{
-    PixelCtx pc;
-    pc.npix = (size_t)P.rows * P.width;
-    if (P.scatterWaves) {
-        // scattered mapping: lane k of wave w takes local pixel k * waves + w, so every wave holds
-        // pixels from the whole tile of rows and all waves cost about the same
-        const size_t li = (size_t)lane * P.scatterWaves + tile;
-        pc.valid = tile < P.scatterWaves && li < pc.npix;
-        pc.li = pc.valid ? li : 0;
-        const uint32_t ly = (uint32_t)(pc.li / P.width);
-        pc.px = (uint32_t)(pc.li - (size_t)ly * P.width);
-        pc.py = global_row(ly, P.rowOffset, P.rowStride, P.bandShift);
-        return pc;
-    }
-    const uint32_t tileX = tile & 0xffffu, tileY = tile >> 16;   // packed (order entries)
-    pc.px = tileX * 8u + (lane & 7u);
-    const uint32_t ly = tileY * 8u + (lane >> 3);
-    pc.valid = tileY < P.tilesY && pc.px < P.width && ly < P.rows;
-    pc.py = global_row(ly, P.rowOffset, P.rowStride, P.bandShift);
-    pc.li = (size_t)ly * P.width + pc.px;
-    return pc;
-}
-
-template <bool AUX>
-PT_DEV void load_pixel(const TraceParams& P, const PixelCtx& pc, Xorwow& rng, PathState& ps, uint32_t accL)
-{
-    // AUX: resume launches (see ssg_fold_kernel; pixels the fold finished are skipped by the caller)
-    rng.d = P.rng[pc.li];
-    rng.v0 = P.rng[pc.npix + pc.li];
-    rng.v1 = P.rng[2 * pc.npix + pc.li];
-    rng.v2 = P.rng[3 * pc.npix + pc.li];
-    rng.v3 = P.rng[4 * pc.npix + pc.li];
-    rng.v4 = P.rng[5 * pc.npix + pc.li];
-    ps.acc = accL;
-    if (!P.ignoreFirst || (AUX && P.fold)) {     // the first call of an ignoreHistory launch overwrites it
-        const float4 a = P.accum[pc.li];
-        float* l = lds_f() + accL;
-        l[0] = a.x;
-        l[64] = a.y;
-        l[128] = a.z;
-    }
-    ps.color = splat(0.0f);
-    ps.L = splat(0.0f);
-    ps.T = splat(1.0f);
-    ps.s = ps.c = ps.bounce = 0;
-    ps.alive = P.chunks > 0 && P.spp > 0;
-    if (AUX && P.fold) {                         // mid-launch state left by ssg_fold_kernel
-        const uint32_t* F = P.fold;
-        ps.color = mk(__uint_as_float(F[(F_COL + 0) * pc.npix + pc.li]), __uint_as_float(F[(F_COL + 1) * pc.npix + pc.li]),
-                      __uint_as_float(F[(F_COL + 2) * pc.npix + pc.li]));
-        const uint32_t sc = F[F_SC * pc.npix + pc.li];
-        ps.s = sc & 0xffffu;
-        ps.c = sc >> 16;
-        ps.alive = ps.c < P.chunks;
-    }
-}
-
-PT_DEV void store_pixel(const TraceParams& P, const PixelCtx& pc, const Xorwow& rng, const PathState& ps)
-{
-    // The pixel index passes through an empty asm so the store addresses are recomputed here from
-    // one 32-bit register: otherwise the compiler reuses the seven 64-bit addresses of load_pixel and
-    // keeps them live (spilled) across the whole tile.  Contexts hold < 2^30 pixels (pt_create).
-    uint32_t li = (uint32_t)pc.li;
-    asm volatile("" : "+v"(li));
-    P.rng[li] = rng.d;
-    P.rng[pc.npix + li] = rng.v0;
-    P.rng[2 * pc.npix + li] = rng.v1;
-    P.rng[3 * pc.npix + li] = rng.v2;
-    P.rng[4 * pc.npix + li] = rng.v3;
-    P.rng[5 * pc.npix + li] = rng.v4;
-    const float* a = lds_f() + ps.acc;
-    P.accum[li] = make_float4(a[0], a[64], a[128], 1.0f);   // trace.cu:198, once per launch
-}
-
 // ---------------------------------------------------------------------------------------------
 // Kernel A: lane-synchronous segments (traverse, then shade), per-lane path regeneration.
 // LDS layout per workgroup: [scene nodes (2 float4 each) | scene prims (4 float4 each)] when
@@ -1488,7 +1555,16 @@ PT_DEV void store_pixel(const TraceParams& P, const PixelCtx& pc, const Xorwow& 
 template <bool STATS, int SL, int WPB, int WW, int MINW, bool PERSIST = false, int MODE = 0>
 __global__ void __launch_bounds__(WPB * 64, MINW) trace_kernel(TraceParams P)
 {
-    constexpr bool SSG = MODE == 1, AUX = MODE == 2, STRIP = MODE == 3;
+    // MODE 4 (AHEAD): run-ahead across render() calls.  A launch of one or a few render() calls ends a
+    // tile when its slowest pixel has finished; the lanes whose pixels finished first would idle until
+    // then (28 % of lane time at 8 spp per call).  Here a lane whose pixel has finished
+    // its last call stores the pixel (the call's final RNG state and accumulation value) and goes on
+    // with the pixel's NEXT call -- the same XORWOW stream -- stashing after every sample the colour
+    // sum so far, the sample count and the state (ahead_store), until the tile ends or a whole next
+    // call is done.  The next launch consumes the stash when its camera and scene are the ones it was
+    // made with (host key, render_impl); otherwise the stored state is the exact one to continue from.
+    // A wave leaves the tile as soon as no lane has samples of this launch left.
+    constexpr bool SSG = MODE == 1, AUX = MODE == 2, STRIP = MODE == 3, AHEAD = MODE == 4;
     const uint32_t lane = threadIdx.x & 63u;
     const uint32_t wave = threadIdx.x >> 6;
     const float4* gnodes = WW >= 3 ? P.cnodes : P.nodes;
@@ -1537,7 +1613,8 @@ __global__ void __launch_bounds__(WPB * 64, MINW) trace_kernel(TraceParams P)
         PathState ps;
         SsgLane sl;
         if (SSG) ssg_load(P, pos, grp, lane, pc.li, pc.npix, rng, ps, sl);
-        else load_pixel<AUX>(P, pc, rng, ps, accL);
+        else load_pixel<AUX, AHEAD>(P, pc, rng, ps, accL);
+        if (AHEAD && ps.s == P.spp) end_call<true>(P, pc, ps, rng);   // a whole call was stashed
         float fx = (float)(int32_t)pc.px, fy = (float)(int32_t)pc.py;
         camera_ray(P, fx, fy, rng, ps.o, ps.d);
         uint32_t stripK = 0;                     // STRIP: this lane's tile within the unit
@@ -1557,6 +1634,7 @@ __global__ void __launch_bounds__(WPB * 64, MINW) trace_kernel(TraceParams P)
             bool fresh = true, held = false;
             TravState ts = {0u, 0u, 0xffffffffu, kFltMax};
             while (ps.alive) {
+                if (AHEAD && __ballot(ps.c < P.chunks) == 0ull) break;   // only run-ahead lanes left
                 if (STATS && fresh && !held) { cnt.segments++; wave_tick(cnt.w_segments); }
                 bool tdone = true;
                 if (!held) {
@@ -1579,7 +1657,7 @@ __global__ void __launch_bounds__(WPB * 64, MINW) trace_kernel(TraceParams P)
                 uint64_t tS = STATS ? __builtin_amdgcn_s_memtime() : 0;
                 if (shade<STATS>(P, prims, ts.elem, ts.tMax, ps, rng, cnt)) {
                     if (SSG) ssg_finish<STATS>(P, ps, rng, fx, fy, sl, lane, pc.li, cnt);
-                    else finish_path<STATS>(P, ps, rng, fx, fy, cnt);
+                    else finish_path<STATS, AHEAD>(P, ps, rng, fx, fy, cnt, pc);
                     if (STRIP && !ps.alive && stripK + 1 < P.strip) {
                         // Strip units (launches of few samples per pixel): a lane whose pixel is done
                         // stores it and takes the same position in the unit's next tile -- the tile to
@@ -1610,7 +1688,7 @@ __global__ void __launch_bounds__(WPB * 64, MINW) trace_kernel(TraceParams P)
             uint64_t tS = STATS ? __builtin_amdgcn_s_memtime() : 0;
             if (shade<STATS>(P, prims, e, t, ps, rng, cnt)) {
                 if (SSG) ssg_finish<STATS>(P, ps, rng, fx, fy, sl, lane, pc.li, cnt);
-                else finish_path<STATS>(P, ps, rng, fx, fy, cnt);
+                else finish_path<STATS>(P, ps, rng, fx, fy, cnt, pc);
             }
             if (STATS) wave_time(cnt.cyc_shade, tS);
         }
@@ -1622,6 +1700,7 @@ __global__ void __launch_bounds__(WPB * 64, MINW) trace_kernel(TraceParams P)
         }
         if (STATS) wave_time(cnt.cyc_total, tAll);
         if (SSG) P.ssgCount[(size_t)sl.logItem * 64 + lane] = sl.k;
+        else if (AHEAD) {}                    // stored when its last call ended (end_call)
         else if (!P.discard) store_pixel(P, pc, rng, ps);
         else if (AUX && P.pairsOut)           // cost pre-pass: draw pairs per sample of this pixel
         {
@@ -2047,6 +2126,16 @@ struct pt_context {
     uint32_t cnodeCount = 0, rootWord = 0;
     bool dfsOrder = true;             // leaves hold their primitives in DFS order (repair_pending)
     bool riseRepair = true;           // pt_set_rise_repair (tests' negative control only)
+    // run-ahead across render() calls (MODE 4): the stash and the key it was made under
+    uint32_t* ahead = nullptr;        // [kAheadWords][pixels]
+    bool aheadValid = false;          // the last launch made a stash
+    pt_camera aheadCam = {};
+    uint64_t aheadState = 0;          // stateEpoch when it was made
+    uint32_t aheadMisses = 0;         // consecutive launches that could not use the previous stash
+    int aheadMode = 0;                // pt_set_run_ahead: 0 automatic, 1 off, 2 always make a stash
+    uint64_t stateEpoch = 0;          // bumped by every change of scene, textures, sky or RNG state
+    uint64_t lastState = 0;           // stateEpoch at the last launch
+    bool launched = false;
     float rootBox[6] = {};
     uint32_t nodeCount = 0, primCount = 0, stackDepth = 1;
     bool slabFast = true;
@@ -2141,8 +2230,10 @@ static hipError_t launch_one(const TraceParams& P, hipStream_t stream)
     const size_t lds = sceneBytes + (size_t)WPB * P.stackDepth * 64 * (WW >= 3 ? 8 : 4) + (size_t)WPB * 64 * 12;
     // no child-box layout: the node-at-a-time walk -- except for grouped and strip launches, whose
     // item and strip hand-off logic lives only in the resumable walk (pick_variant never sends them here)
-    if (WW >= 3 && P.cnodes == nullptr)
-        return (MODE == 1 || MODE == 3) ? hipErrorInvalidValue : launch_one<STATS, SL, WPB, 1, MINW, PERSIST, MODE>(P, stream);
+    if (WW >= 3 && P.cnodes == nullptr) {
+        if constexpr (MODE == 1 || MODE >= 3) return hipErrorInvalidValue;
+        else return launch_one<STATS, SL, WPB, 1, MINW, PERSIST, MODE>(P, stream);
+    }
     if (lds > 160 * 1024) {
         // scene too large to stage in LDS: the same variant reading the scene through the caches
         if (SL > 0) return launch_one<STATS, 0, WPB, WW, MINW, PERSIST, MODE>(P, stream);
@@ -2259,6 +2350,17 @@ static hipError_t launch_strip(int v, const TraceParams& P, hipStream_t stream)
 
 static bool strip_capable(int v) { return v == 40 || v == 41 || v == 46; }
 
+// Run-ahead launches (MODE 4) of the resumable persistent variants.
+static hipError_t launch_ahead(int v, const TraceParams& P, hipStream_t stream)
+{
+    switch (v) {
+    case 40: return launch_one<false, 1, 4, kV40Walk, 5, true, 4>(P, stream);
+    case 41: return launch_one<false, 0, 4, 14212, 5, true, 4>(P, stream);
+    case 46: return launch_one<false, 0, 4, 14212, 4, true, 4>(P, stream);
+    default: return hipErrorInvalidValue;
+    }
+}
+
 // Tiles per dispatch unit.  A launch of few samples per pixel idles the lanes whose pixels finish
 // first for the rest of their tile; strips of K tiles let those lanes go on with the next tile.
 // Measured at 1080p (tools/call_loop.py, profiles/r04_call_loop.json): 1-spp progressive frames
@@ -2288,6 +2390,10 @@ static bool variant_shipped(int v)
 
 // Cost pre-pass of a cold-start launch (render_impl): samples per pixel, and the smallest launch
 // (spp x chunks) that gets one.
+// Run-ahead (MODE 4): launches of kAheadMinSamples..kAheadMaxSamples samples per pixel make a stash
+// of the next call's first samples (the reference's render(cam, 8, ...) calls, main.cpp:272-279);
+// 1-2 spp progressive frames use strip units instead.
+constexpr uint64_t kAheadMinSamples = 3, kAheadMaxSamples = 64;
 constexpr uint32_t kPrepassSpp = 2;
 constexpr uint64_t kPrepassMinSpp = 16;
 
@@ -2450,6 +2556,7 @@ PT_API void pt_destroy(pt_context* ctx)
     (void)hipFree(ctx->patchLog);
     (void)hipFree(ctx->patchEnd);
     (void)hipFree(ctx->patchCount);
+    (void)hipFree(ctx->ahead);
     for (auto& t : ctx->hostTex) (void)hipFree((void*)t.texels);
     if (ctx->ev0) (void)hipEventDestroy(ctx->ev0);
     if (ctx->ev1) (void)hipEventDestroy(ctx->ev1);
@@ -2585,6 +2692,7 @@ PT_API int pt_set_scene(pt_context* ctx, const pt_bvh_node* nodes, uint32_t node
     }
     ctx->dfsOrder = dfsOrder;
     ctx->orderStale = true;
+    ++ctx->stateEpoch;
     ctx->rootWord = word(0);
     for (int k = 0; k < 3; ++k) {
         ctx->rootBox[2 * k] = nodes[0].aabb_min[k];
@@ -2643,6 +2751,7 @@ PT_API int pt_set_texture(pt_context* ctx, uint32_t handle, const float* rgba, u
     t.fwidth = (float)width;
     t.fheight = (float)height;
     ctx->orderStale = true;
+    ++ctx->stateEpoch;
     PT_HIP_CHECK(ctx, hipMemcpy(ctx->texTable, ctx->hostTex, sizeof(ctx->hostTex), hipMemcpyHostToDevice));
     return PT_OK;
 }
@@ -2651,6 +2760,7 @@ PT_API int pt_set_skybox(pt_context* ctx, uint32_t handle)
 {
     if (!ctx) return PT_ERR_ARG;
     if (handle > PT_MAX_TEXTURES) return fail(ctx, PT_ERR_ARG, "pt_set_skybox: invalid handle");
+    if (ctx->skybox != handle) ++ctx->stateEpoch;
     ctx->skybox = handle;
     return PT_OK;
 }
@@ -2966,6 +3076,17 @@ static int render_impl(pt_context* ctx, const pt_camera* cam, uint32_t spp, uint
         ctx->orderTiles = tiles;
         ctx->orderStale = true;
     }
+    // Run-ahead across render() calls (MODE 4): a stash made by the previous launch is valid when
+    // this launch has its camera, scene, textures, sky and RNG state (stateEpoch); a context whose
+    // camera or state changed on the last two launches (a moving progressive camera) stops making
+    // stashes until it holds still again.
+    const bool sameKey = ctx->launched && memcmp(&ctx->lastCam, cam, sizeof(pt_camera)) == 0 &&
+                         ctx->lastState == ctx->stateEpoch;
+    ctx->aheadMisses = sameKey ? 0u : std::min(ctx->aheadMisses + 1u, 1000u);
+    const bool stashMatches = ctx->aheadValid && sameKey;
+    ctx->aheadValid = false;              // consumed or dropped; a making launch sets it again
+    ctx->launched = true;
+    ctx->lastState = ctx->stateEpoch;
     if (memcmp(&ctx->lastCam, cam, sizeof(pt_camera)) != 0) {
         ctx->orderStale = true;
         ctx->lastCam = *cam;
@@ -2975,7 +3096,13 @@ static int render_impl(pt_context* ctx, const pt_camera* cam, uint32_t spp, uint
     // tiles, and a lane whose pixel is done moves on to the next tile of its strip.  The cost order
     // is over units, so it is rebuilt when K changes.
     const bool noRepair = !ctx->riseRepair;           // test knob: plain launches of variant 90 only
-    const uint32_t K = (sorted && !stats && !noRepair) ? strip_tiles(ctx, pick_variant(ctx), tiles, (uint64_t)spp * chunks) : 1u;
+    const uint64_t launchSamples = (uint64_t)spp * chunks;
+    const bool aheadCapable = !stats && !noRepair && ctx->cnodes && strip_capable(pick_variant(ctx)) && ctx->aheadMode != 1;
+    const bool aheadUse = aheadCapable && stashMatches;
+    const bool aheadMake = aheadCapable && (ctx->aheadMode == 2 ||
+        (launchSamples >= kAheadMinSamples && launchSamples <= kAheadMaxSamples && ctx->aheadMisses < 2));
+    const bool ahead = aheadUse || aheadMake;
+    const uint32_t K = (sorted && !stats && !noRepair && !ahead) ? strip_tiles(ctx, pick_variant(ctx), tiles, launchSamples) : 1u;
     const uint32_t unitsX = (P.tilesX + K - 1) / K, units = unitsX * P.tilesY;
     if (K != ctx->orderStrip) {
         ctx->orderValid = false;
@@ -3024,8 +3151,17 @@ static int render_impl(pt_context* ctx, const pt_camera* cam, uint32_t spp, uint
     const uint32_t total = spp * chunks;
     // the fold state packs (sample in call, call) into one word as sIdx | c << 16 (ssg_fold_kernel)
     const bool groupable = !stats && sorted && (uint64_t)spp * chunks < (1ull << 31) && spp <= 0xffffu && chunks <= 0xffffu;
-    uint32_t G = groupable && K == 1 && !noRepair ? ssg_groups(ctx, variant, tiles, total) : 0;
-    if (!G && ctx->variant == 0 && K == 1 && !noRepair) variant = small_grid_variant(ctx, variant, tiles);
+    uint32_t G = groupable && K == 1 && !noRepair && !ahead ? ssg_groups(ctx, variant, tiles, total) : 0;
+    if (!G && ctx->variant == 0 && K == 1 && !noRepair && !ahead) variant = small_grid_variant(ctx, variant, tiles);
+    if (ahead) {
+        if (!ctx->ahead) {
+            const size_t n = std::max<size_t>((size_t)ctx->rows * ctx->width, 1);
+            PT_HIP_CHECK(ctx, hipMalloc(&ctx->ahead, kAheadWords * n * sizeof(uint32_t)));
+        }
+        P.ahead = ctx->ahead;
+        P.aheadUse = aheadUse ? 1u : 0u;
+        P.aheadMake = aheadMake ? 1u : 0u;
+    }
     if (noRepair) {
         if (variant != 40 || stats)
             return fail(ctx, PT_ERR_STATE, "pt_set_rise_repair(0): only plain launches of variant 40 have a no-repair build");
@@ -3087,7 +3223,13 @@ static int render_impl(pt_context* ctx, const pt_camera* cam, uint32_t spp, uint
         ctx->lastGroups = G;
     } else {
         PT_HIP_CHECK(ctx, stats ? launch_variant<true>(variant, P, ctx->stream)
+                                : ahead ? launch_ahead(variant, P, ctx->stream)
                                 : (K > 1 ? launch_strip(variant, P, ctx->stream) : launch_variant<false>(variant, P, ctx->stream)));
+    }
+    if (aheadMake) {
+        ctx->aheadValid = true;
+        ctx->aheadCam = *cam;
+        ctx->aheadState = ctx->stateEpoch;
     }
     PT_HIP_CHECK(ctx, hipGetLastError());
     PT_HIP_CHECK(ctx, hipEventRecord(ctx->ev1, ctx->stream));
@@ -3130,6 +3272,13 @@ static int render_impl(pt_context* ctx, const pt_camera* cam, uint32_t spp, uint
         stats->family_execs_compacted_in_round = h[21];
         stats->repairs = h[22];
     }
+    return PT_OK;
+}
+
+PT_API int pt_set_run_ahead(pt_context* ctx, int mode)
+{
+    if (!ctx || mode < 0 || mode > 2) return PT_ERR_ARG;
+    ctx->aheadMode = mode;
     return PT_OK;
 }
 
@@ -3314,6 +3463,7 @@ PT_API int pt_write_rng(pt_context* ctx, const uint32_t* src)
     for (size_t i = 0; i < npix; ++i)
         for (int k = 0; k < 6; ++k) soa[k * npix + i] = src[6 * i + k];
     PT_HIP_CHECK(ctx, hipMemcpy(ctx->rng, soa.data(), soa.size() * sizeof(uint32_t), hipMemcpyHostToDevice));
+    ++ctx->stateEpoch;                    // a run-ahead stash continues the old streams: void
     return PT_OK;
 }
 

@@ -112,3 +112,25 @@ def insert_orphan(nodes: Sequence[Node], p: int) -> List[Node]:
             out.append((lo, hi, nodes[p][2] + 1, pca & 0xFF00))   # orphan: first child p + 1 (= old p)
         out.append((lo, hi, (off + 1 if off >= p else off) if (pca >> 16) == 0 else off, pca))
     return out
+
+
+def rise_pair_bvh(aabbs) -> Tuple[List[Node], List[int]]:
+    """Caller BVH over scenes/rise_pair.scene.json's objects (file order: 0 dome, 1 sphere A, 2 wall B
+    behind A; camera looking down -z), returns (nodes, object index of each primitive slot):
+
+        0 R  split z -> first 1 (N), second 4 (leaf A)      d.z < 0: near = second = A
+        1 N  split z -> first 2 (leaf B), second 3 (leaf dome)   near = second = dome
+        2 leaf B   3 leaf dome   4 leaf A                    primitives [B, dome, A]: DFS order
+
+    A ray that hits A: R pushes N, A's leaf sets t_max = tA; N is popped, its far child B fails at tA
+    (B lies behind A) and is not kept by the hit-now rule, the dome's leaf returns its far root t1 >
+    tA (Hittable.inl:152-158, the ray starts inside) and RAISES t_max; the reference then pops B's
+    leaf, which passes at t1, and B's hit at tB < t1 wins (trace.cu:48-98).  Without the rebuild of
+    the pending set the dome would win."""
+    box = [(tuple(a[:3]), tuple(a[3:])) for a in aabbs]
+    order = [2, 0, 1]                                         # slots: B, dome, A
+    leaf = {o: (box[o][0], box[o][1], slot, 1 << 16) for slot, o in enumerate(order)}
+    n_lo, n_hi = _union([box[2], box[0]])
+    r_lo, r_hi = _union([box[0], box[1], box[2]])
+    nodes = [(r_lo, r_hi, 4, 2 << 8), (n_lo, n_hi, 3, 2 << 8), leaf[2], leaf[0], leaf[1]]
+    return nodes, order

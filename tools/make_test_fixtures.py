@@ -9,7 +9,12 @@
                                  sphere, so the sphere test's far-root quirk (Hittable.inl:152-158,
                                  t1 accepted beyond t_max when t0 <= t_min) raises t_max in mid
                                  traversal and the reference then tests popped boxes at the larger
-                                 value (trace.cu:48-98) -- the case repair_pending exists for.
+                                 value (trace.cu:48-98) -- the case repair_pending exists for;
+  scenes/rise_pair.scene.json    three objects -- a dome sphere around the camera, a sphere A and a
+                                 back wall B behind it -- for the caller BVH of tests/bvh_edit.py
+                                 rise_pair_bvh(), in which every ray that hits A raises t_max at the
+                                 dome's leaf with B's leaf dropped by the hit-now rule: the pixels of
+                                 A then differ unless the pending set is rebuilt.
 """
 import json
 import pathlib
@@ -98,11 +103,22 @@ def rise_scene() -> dict:
     return {"camera": {"position": [0.0, 1.3, 4.0], "look_at": [0.0, 0.6, 0.0], "fovy": 50.0}, "objects": objs}
 
 
+def rise_pair_scene() -> dict:
+    return {"camera": {"position": [0.0, 1.0, 4.0], "look_at": [0.0, 1.0, 0.0], "fovy": 45.0},
+            "objects": [obj("SPHERE", (0.0, 1.0, 0.0), (0.0, 0.0, 0.0), (8.0, 8.0, 8.0), "LAMBERT", (0.6, 0.6, 0.7),
+                            emissive=(0.5, 0.5, 0.6)),
+                        obj("SPHERE", (0.0, 1.0, 0.0), (0.0, 0.0, 0.0), (0.6, 0.6, 0.6), "LAMBERT", (0.9, 0.2, 0.2)),
+                        obj("QUAD", (0.0, 1.0, -2.0), (-90.0, 0.0, 0.0), (3.0, 3.0, 3.0), "LAMBERT", (0.2, 0.8, 0.3),
+                            emissive=(0.2, 0.6, 0.2))]}
+
+
 def main() -> int:
     checker_png(ROOT / "scenes" / "checker.png")
     (ROOT / "scenes" / "test_shapes.scene.json").write_text(json.dumps(scene(), indent=1) + "\n")
     (ROOT / "scenes" / "rise_repair.scene.json").write_text(json.dumps(rise_scene(), indent=1) + "\n")
-    print("wrote scenes/checker.png, scenes/test_shapes.scene.json, scenes/rise_repair.scene.json")
+    (ROOT / "scenes" / "rise_pair.scene.json").write_text(json.dumps(rise_pair_scene(), indent=1) + "\n")
+    print("wrote scenes/checker.png, scenes/test_shapes.scene.json, scenes/rise_repair.scene.json, "
+          "scenes/rise_pair.scene.json")
     return 0
 
 
