@@ -3097,7 +3097,9 @@ static int render_impl(pt_context* ctx, const pt_camera* cam, uint32_t spp, uint
     // is over units, so it is rebuilt when K changes.
     const bool noRepair = !ctx->riseRepair;           // test knob: plain launches of variant 90 only
     const uint64_t launchSamples = (uint64_t)spp * chunks;
-    const bool aheadCapable = !stats && !noRepair && ctx->cnodes && strip_capable(pick_variant(ctx)) && ctx->aheadMode != 1;
+    // (strip units or sample groups forced by their knobs take precedence over automatic run-ahead)
+    const bool aheadCapable = !stats && !noRepair && ctx->cnodes && strip_capable(pick_variant(ctx)) && ctx->aheadMode != 1 &&
+                              (ctx->aheadMode == 2 || (ctx->stripMode < 2 && ctx->ssgMode < 2));
     const bool aheadUse = aheadCapable && stashMatches;
     const bool aheadMake = aheadCapable && (ctx->aheadMode == 2 ||
         (launchSamples >= kAheadMinSamples && launchSamples <= kAheadMaxSamples && ctx->aheadMisses < 2));
