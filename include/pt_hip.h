@@ -261,6 +261,11 @@ PT_API int pt_set_rise_repair(pt_context *ctx, int enabled);
  * way.  0 = automatic (the default; stops while the camera or scene changes at every launch),
  * 1 = off, 2 = make a stash at every launch (tests). */
 PT_API int pt_set_run_ahead(pt_context *ctx, int mode);
+/* Tuning knob of the cold start (the first launch after a scene, texture or camera change, which has
+ * no tile costs yet): samples per pixel of the cost pre-pass (0 = default 2, at most 64) and whether
+ * the launch runs with issue priority on the pre-pass's order (0 = no, the default; 1 = yes).
+ * Scheduling only: results are identical for every setting. */
+PT_API int pt_set_cold_start(pt_context *ctx, uint32_t prepass_spp, int priority);
 PT_API int pt_set_sample_groups(pt_context *ctx, int mode);
 PT_API int pt_set_patch_rounds(pt_context *ctx, uint32_t rounds);
 PT_API int pt_set_group_lookback(pt_context *ctx, uint32_t far, uint32_t near);

@@ -328,6 +328,12 @@ class Pathtracer:
         for c in self._contexts():
             N.check_ctx(N.hip().pt_set_run_ahead(c, int(mode)), c)
 
+    def set_cold_start(self, prepass_spp: int = 0, priority: bool = False) -> None:
+        """Cold-start scheduling (pt_set_cold_start): cost pre-pass spp (0 = default) and issue
+        priority on the pre-pass's order.  Results are identical for every setting."""
+        for c in self._contexts():
+            N.check_ctx(N.hip().pt_set_cold_start(c, int(prepass_spp), int(bool(priority))), c)
+
     def set_rise_repair(self, enabled: bool) -> None:
         """Test knob (pt_set_rise_repair): False skips the rebuild of the pending far children after a
         leaf raised t_max, so results are NOT the reference's on such rays (negative control)."""

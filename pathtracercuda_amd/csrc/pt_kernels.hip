@@ -2167,6 +2167,8 @@ struct pt_context {
     uint64_t aheadState = 0;          // stateEpoch when it was made
     uint32_t aheadMisses = 0;         // consecutive launches that could not use the previous stash
     int aheadMode = 0;                // pt_set_run_ahead: 0 automatic, 1 off, 2 always make a stash
+    uint32_t prepassSpp = 0;          // pt_set_cold_start: cost pre-pass samples per pixel (0 = kPrepassSpp)
+    bool coldPriority = false;        // pt_set_cold_start: issue priority on the pre-pass's order
     uint64_t stateEpoch = 0;          // bumped by every change of scene, textures, sky or RNG state
     uint64_t lastState = 0;           // stateEpoch at the last launch
     bool launched = false;
@@ -3238,7 +3240,7 @@ static int render_impl(pt_context* ctx, const pt_camera* cam, uint32_t spp, uint
         // Progressive 1-spp frames skip it and reuse the previous order for one launch instead.
         TraceParams Q = P;
         const bool guesses = G != 0;           // speculative groups also take their offset guesses from it
-        Q.spp = guesses ? 8u : kPrepassSpp;
+        Q.spp = guesses ? 8u : (ctx->prepassSpp ? ctx->prepassSpp : kPrepassSpp);
         Q.chunks = 1;
         Q.ignoreFirst = 1;
         Q.discard = 1;
@@ -3251,6 +3253,7 @@ static int render_impl(pt_context* ctx, const pt_camera* cam, uint32_t spp, uint
         const int rs = sort_order(ctx, tiles, Q.spp, K);
         if (rs != PT_OK) return rs;
         P.order = ctx->order;
+        if (ctx->coldPriority && ctx->prioMode == 0) issue_priority(ctx, units, P.prio);
     }
     if (G && P.tileCost) PT_HIP_CHECK(ctx, hipMemsetAsync(P.tileCost, 0, (size_t)tiles * sizeof(uint32_t), ctx->stream));
     if (G) {
@@ -3308,6 +3311,14 @@ static int render_impl(pt_context* ctx, const pt_camera* cam, uint32_t spp, uint
         stats->family_execs_compacted_in_round = h[21];
         stats->repairs = h[22];
     }
+    return PT_OK;
+}
+
+PT_API int pt_set_cold_start(pt_context* ctx, uint32_t prepass_spp, int priority)
+{
+    if (!ctx || prepass_spp > 64 || priority < 0 || priority > 1) return PT_ERR_ARG;
+    ctx->prepassSpp = prepass_spp;
+    ctx->coldPriority = priority != 0;
     return PT_OK;
 }
 
