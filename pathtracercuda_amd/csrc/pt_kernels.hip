@@ -2355,6 +2355,7 @@ static hipError_t launch_variant(int v, const TraceParams& P, hipStream_t stream
     case 47: return launch_one<STATS, 1, 4, 224, 4, true, MODE>(P, stream);
     case 48: return launch_one<STATS, 2, 4, 13216, 4, true, MODE>(P, stream);
     case 90: return launch_one<false, 1, 4, 100000 + kV40Walk, 5, true, 0>(P, stream);   // test only: 40, no repair
+    case 91: return launch_one<false, 2, 4, 113216, 4, true, 0>(P, stream);              // A/B only: 48, no repair
     default: return hipErrorInvalidValue;
     }
 }
@@ -2421,7 +2422,8 @@ static uint32_t strip_tiles(const pt_context* ctx, int variant, uint32_t tiles, 
 
 static bool variant_shipped(int v)
 {
-    return v == 0 || v == 1 || v == 4 || v == 6 || v == 20 || v == 40 || v == 41 || v == 46 || v == 47 || v == 48 || v == 39;
+    return v == 0 || v == 1 || v == 4 || v == 6 || v == 20 || v == 40 || v == 41 || v == 46 || v == 47 || v == 48 || v == 39 ||
+           v == 91;   // 91: variant 48 without the rising-t_max rebuild (A/B of its cost only; not the reference's bits)
 }
 
 // Cost pre-pass of a cold-start launch (render_impl): samples per pixel, and the smallest launch

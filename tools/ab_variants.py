@@ -27,6 +27,7 @@ def main():
     ap.add_argument("--n", type=int, default=1, help="render one rank's share of an N-way 8-row band partition")
     ap.add_argument("--rank", type=int, default=0)
     ap.add_argument("--groups", type=int, default=1, help="sample groups: 1 = off (plain launches), 0 = automatic")
+    ap.add_argument("--check", type=int, default=1, help="assert every variant bit-identical (0 for A/B-only variants)")
     a = ap.parse_args()
     if a.scene == "stress_100k":                   # C5's generated scene (bench.scene_path)
         import bench
@@ -50,7 +51,7 @@ def main():
         pt.set_rng_state(st)
         if ref is None:
             ref = acc
-        assert np.array_equal(acc.view(np.uint32), ref.view(np.uint32)), f"variant {v} schedule {m} differs"
+        assert not a.check or np.array_equal(acc.view(np.uint32), ref.view(np.uint32)), f"variant {v} schedule {m} differs"
     for r in range(a.rounds):
         for v, m in vs:
             pt.set_kernel_variant(v)
