@@ -8,6 +8,7 @@ chunking).
 """
 import numpy as np
 import pytest
+import torch  # noqa: F401 -- before the native libraries: one HIP runtime per process
 
 import pathtracercuda_amd as pa
 from oracle import pyoracle as po
