@@ -261,7 +261,8 @@ PT_API int pt_set_rise_repair(pt_context *ctx, int enabled);
  * way.  Once the tile queue of a launch is empty, a wave goes back to the tiles it finished and
  * continues their run-ahead until every tile of the launch is done (tail fill).
  * 0 = automatic (the default; stops while the camera or scene changes at every launch),
- * 1 = off, 2 = make a stash at every launch (tests), 3 = automatic without the tail fill (A/B). */
+ * 1 = off, 2 = make a stash at every launch (tests), 3 = automatic without the tail fill (A/B),
+ * 4 = make stashes but never use them (diagnostic: the cost of the run-ahead work alone). */
 PT_API int pt_set_run_ahead(pt_context *ctx, int mode);
 /* Tuning knob of the cold start (the first launch after a scene, texture or camera change, which has
  * no tile costs yet): samples per pixel of the cost pre-pass (0 = default 2, at most 64) and whether

@@ -1297,8 +1297,11 @@ PT_DEV void ahead_resume(const TraceParams& P, const PixelCtx& pc, Xorwow& rng, 
 // finished so far, counted in the persistent cursor's third word.
 PT_DEV bool ahead_all_done(const TraceParams& P)
 {
-    const uint32_t d = __hip_atomic_load(P.tileCursor + 2, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    return __builtin_amdgcn_readfirstlane(d) >= P.numSlots;
+    // an atomic RMW, not a load: a plain (even atomic) load may be served by this XCD's L2 copy
+    const uint32_t lane = threadIdx.x & 63u;
+    uint32_t d = 0;
+    if (lane == (uint32_t)(__ffsll((long long)__ballot(1)) - 1)) d = atomicAdd(P.tileCursor + 2, 0u);
+    return __builtin_amdgcn_readfirstlane(__builtin_amdgcn_readlane(d, __ffsll((long long)__ballot(1)) - 1)) >= P.numSlots;
 }
 
 PT_DEV void store_pixel(const TraceParams& P, const PixelCtx& pc, const Xorwow& rng, const PathState& ps)
@@ -3201,7 +3204,7 @@ static int render_impl(pt_context* ctx, const pt_camera* cam, uint32_t spp, uint
     // (strip units or sample groups forced by their knobs take precedence over automatic run-ahead)
     const bool aheadCapable = !stats && !noRepair && ctx->cnodes && strip_capable(pick_variant(ctx)) && ctx->aheadMode != 1 &&
                               (ctx->aheadMode == 2 || (ctx->stripMode < 2 && ctx->ssgMode < 2));
-    const bool aheadUse = aheadCapable && stashMatches;
+    const bool aheadUse = aheadCapable && stashMatches && ctx->aheadMode != 4;   // 4: diagnostic, never consume
     const bool aheadMake = aheadCapable && (ctx->aheadMode == 2 ||
         (launchSamples >= kAheadMinSamples && launchSamples <= kAheadMaxSamples && ctx->aheadMisses < 2));
     const bool ahead = aheadUse || aheadMake;
@@ -3264,7 +3267,7 @@ static int render_impl(pt_context* ctx, const pt_camera* cam, uint32_t spp, uint
         P.ahead = ctx->ahead;
         P.aheadUse = aheadUse ? 1u : 0u;
         P.aheadMake = aheadMake ? 1u : 0u;
-        P.aheadTail = ctx->aheadMode == 3 ? 0u : 1u;
+        P.aheadTail = (ctx->aheadMode == 3 || ctx->aheadMode == 4) ? 0u : 1u;
     }
     if (noRepair) {
         if (variant != 40 || stats)
@@ -3390,7 +3393,7 @@ PT_API int pt_set_cold_start(pt_context* ctx, uint32_t prepass_spp, int priority
 
 PT_API int pt_set_run_ahead(pt_context* ctx, int mode)
 {
-    if (!ctx || mode < 0 || mode > 3) return PT_ERR_ARG;
+    if (!ctx || mode < 0 || mode > 4) return PT_ERR_ARG;
     ctx->aheadMode = mode;
     return PT_OK;
 }
