@@ -265,9 +265,11 @@ PT_API int pt_set_rise_repair(pt_context *ctx, int enabled);
  * 4 = make stashes but never use them (diagnostic: the cost of the run-ahead work alone). */
 PT_API int pt_set_run_ahead(pt_context *ctx, int mode);
 /* Tuning knob of the cold start (the first launch after a scene, texture or camera change, which has
- * no tile costs yet): samples per pixel of the cost pre-pass (0 = default 2, at most 64) and whether
- * the launch runs with issue priority on the pre-pass's order (0 = no, the default; 1 = yes).
- * Scheduling only: results are identical for every setting. */
+ * no tile costs yet).  prepass_spp = 0 (default): a launch of several render() calls runs its first
+ * call alone in row-major order and the rest in the cost order of that call (a one-call launch runs a
+ * discarded 2-spp cost pre-pass); prepass_spp > 0 (at most 64): always a discarded pre-pass of that
+ * many spp.  priority: issue priority on that order (1, the default) or not (0).  Scheduling only:
+ * results are identical for every setting. */
 PT_API int pt_set_cold_start(pt_context *ctx, uint32_t prepass_spp, int priority);
 PT_API int pt_set_sample_groups(pt_context *ctx, int mode);
 PT_API int pt_set_patch_rounds(pt_context *ctx, uint32_t rounds);

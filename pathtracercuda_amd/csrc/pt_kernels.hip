@@ -2233,8 +2233,9 @@ struct pt_context {
     uint64_t aheadState = 0;          // stateEpoch when it was made
     uint32_t aheadMisses = 0;         // consecutive launches that could not use the previous stash
     int aheadMode = 0;                // pt_set_run_ahead: 0 automatic, 1 off, 2 always make a stash, 3 = 0 without tail fill
-    uint32_t prepassSpp = 0;          // pt_set_cold_start: cost pre-pass samples per pixel (0 = kPrepassSpp)
-    bool coldPriority = false;        // pt_set_cold_start: issue priority on the pre-pass's order
+    uint32_t prepassSpp = 0;          // pt_set_cold_start: 0 = first call split off (pre-pass of kPrepassSpp for
+                                      // one-call launches), > 0 = a discarded pre-pass of that many spp
+    bool coldPriority = true;         // pt_set_cold_start: issue priority on the cold start's order
     uint64_t stateEpoch = 0;          // bumped by every change of scene, textures, sky or RNG state
     uint64_t lastState = 0;           // stateEpoch at the last launch
     bool launched = false;
@@ -3302,11 +3303,38 @@ static int render_impl(pt_context* ctx, const pt_camera* cam, uint32_t spp, uint
     // of up to ~15 GB): before the timed region starts
     if (!G) ssg_release(ctx);
     PT_HIP_CHECK(ctx, hipEventRecord(ctx->ev0, ctx->stream));
-    if (sorted && (ctx->orderStale || !ctx->orderValid) && (uint64_t)spp * chunks >= kPrepassMinSpp && !stats) {
-        // Cold start (first launch, or the scene, a texture or the camera changed): a short cost
-        // pre-pass measures every tile -- kPrepassSpp samples per pixel from the pixels' current RNG
-        // state, nothing written back (discard) -- and the launch below already runs in cost order.
-        // Progressive 1-spp frames skip it and reuse the previous order for one launch instead.
+    // Cold start (first launch, or the scene, a texture or the camera changed): no tile costs yet.
+    // Progressive 1-spp frames reuse the previous order for one launch.  A launch of several render()
+    // calls runs its FIRST call as a launch of its own in row-major order, sorts the tiles by that
+    // call's costs on the device and runs the other calls in that order -- nothing is computed twice,
+    // and two launches of 1 and chunks - 1 calls are the reference's calls exactly as one launch is
+    // (each call folds into the accumulation, ignoreHistory applies to the first).  Other launches
+    // (one call, or sample groups, which take their draw-pair guesses from it) run a short discarded
+    // pre-pass instead.  Either way the launch then runs with issue priority on that order
+    // (pt_set_cold_start; measured: one-shot C3 251-255 -> 238-240 ms, tools/cold_start.py); as its
+    // tile costs are measured under priority, the order rebuilt from them is biased toward the head's
+    // tiles, so the next launch rebuilds it again without priority (orderSamples = 0 below).
+    const bool cold = sorted && (ctx->orderStale || !ctx->orderValid) && (uint64_t)spp * chunks >= kPrepassMinSpp && !stats;
+    const bool splitCall = cold && chunks >= 2 && !G && K == 1 && !ahead && ctx->prepassSpp == 0;
+    bool biasedOrder = false;
+    if (splitCall) {
+        TraceParams Q = P;
+        Q.chunks = 1;
+        Q.order = firstOrder;
+        for (int i = 0; i < 3; ++i) Q.prio[i] = 0;        // row-major positions: no priority grading
+        PT_HIP_CHECK(ctx, launch_variant<false>(variant, Q, ctx->stream));
+        const int rs = sort_order(ctx, tiles, spp, K);
+        if (rs != PT_OK) return rs;
+        P.order = ctx->order;
+        P.chunks = chunks - 1;
+        P.ignoreFirst = 0;                               // the first call is done
+        if (ctx->coldPriority && ctx->prioMode == 0) {
+            issue_priority(ctx, units, P.prio);
+            biasedOrder = true;
+        }
+    } else if (cold) {
+        // pre-pass: kPrepassSpp samples per pixel from the pixels' current RNG state, nothing
+        // written back (discard)
         TraceParams Q = P;
         const bool guesses = G != 0;           // speculative groups also take their offset guesses from it
         Q.spp = guesses ? 8u : (ctx->prepassSpp ? ctx->prepassSpp : kPrepassSpp);
@@ -3322,7 +3350,10 @@ static int render_impl(pt_context* ctx, const pt_camera* cam, uint32_t spp, uint
         const int rs = sort_order(ctx, tiles, Q.spp, K);
         if (rs != PT_OK) return rs;
         P.order = ctx->order;
-        if (ctx->coldPriority && ctx->prioMode == 0) issue_priority(ctx, units, P.prio);
+        if (ctx->coldPriority && ctx->prioMode == 0) {
+            issue_priority(ctx, units, P.prio);
+            biasedOrder = true;
+        }
     }
     if (G && P.tileCost) PT_HIP_CHECK(ctx, hipMemsetAsync(P.tileCost, 0, (size_t)tiles * sizeof(uint32_t), ctx->stream));
     if (G) {
@@ -3352,6 +3383,7 @@ static int render_impl(pt_context* ctx, const pt_camera* cam, uint32_t spp, uint
     if (sorted && (ctx->orderStale || !ctx->orderValid || total >= 4 * ctx->orderSamples)) {
         const int rs = sort_order(ctx, tiles, total, K);
         if (rs != PT_OK) return rs;
+        if (biasedOrder) ctx->orderSamples = 0;          // costs measured under priority: rebuild once more
     }
     if (stats) {
         unsigned long long h[kStatWords];

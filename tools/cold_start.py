@@ -21,7 +21,7 @@ ap.add_argument("--width", type=int, default=1920)
 ap.add_argument("--height", type=int, default=1080)
 ap.add_argument("--spp", type=int, default=1024)
 ap.add_argument("--reps", type=int, default=2)
-ap.add_argument("--settings", default="2:0,8:0,32:0,2:1,8:1,32:1")
+ap.add_argument("--settings", default="0:1,0:0,2:1,8:1,2:0")
 ap.add_argument("--scene", default=str(ROOT / "scenes/generated_scene.scene.json"))
 a = ap.parse_args()
 samples = a.width * a.height * a.spp
@@ -40,7 +40,7 @@ for rep in range(a.reps):
             ms = [pt.render_raw(cam, 8, a.spp // 8, True)]
         else:
             pre, prio = (int(x) for x in tok.split(":"))
-            pt.set_cold_start(pre, bool(prio))
+            pt.set_cold_start(pre, bool(prio))            # 0:x = first call split off
             ms = [pt.render_raw(cam, 8, a.spp // 8, True)]   # gpu_ms includes the pre-pass
             acc = pt.accum().view(np.uint32).copy()
             if ref is None:
