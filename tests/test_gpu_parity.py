@@ -409,6 +409,18 @@ def test_cold_start_prepass_keeps_results(gpu_available, scenes):
     a.render(cam, 8, False, chunks=2)
     b.render(cam, 8, False, chunks=2)
     assert np.array_equal(bits(a.accum()), bits(b.accum()))
+    # cold launches beyond the run-ahead range: the first render() call split off as a launch of its
+    # own (ignoreHistory on it only), then a one-call launch (discarded pre-pass), each after a camera
+    # change, then warm launches (the order rebuilt once more without priority)
+    for spp, chunks, ignore, move in ((8, 9, True, True), (8, 9, False, False), (32, 3, False, True),
+                                      (72, 1, False, True), (8, 12, False, False), (8, 12, True, False)):
+        if move:
+            pa.camera_rotate(cam, -0.01, 0.02, 0.0)
+        a.render(cam, spp, ignore, chunks=chunks)
+        b.render(cam, spp, ignore, chunks=chunks)
+        assert np.array_equal(bits(a.accum()), bits(b.accum())), (spp, chunks, ignore)
+        assert np.array_equal(a.rng_state(), b.rng_state()), (spp, chunks, ignore)
+        assert a.frames == b.frames
 
 
 def test_tonemap_bitexact(gpu_available, scenes):

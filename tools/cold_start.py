@@ -35,8 +35,9 @@ for rep in range(a.reps):
         cam = pt.load_scene(a.scene)
         st = pt.rng_state()
         if tok == "warm":
-            pt.render_raw(cam, 8, a.spp // 8, True)          # cold launch, order rebuilt from it
-            pt.set_rng_state(st)                              # (a state write keeps the order)
+            for _ in range(2):                                # cold launch, then one that rebuilds the
+                pt.render_raw(cam, 8, a.spp // 8, True)       # order without priority
+                pt.set_rng_state(st)                          # (a state write keeps the order)
             ms = [pt.render_raw(cam, 8, a.spp // 8, True)]
         else:
             pre, prio = (int(x) for x in tok.split(":"))
@@ -46,7 +47,7 @@ for rep in range(a.reps):
             if ref is None:
                 ref = acc
             ok = ok and np.array_equal(acc, ref)
-            for _ in range(2):
+            for _ in range(3):
                 pt.set_rng_state(st)
                 ms.append(pt.render_raw(cam, 8, a.spp // 8, True))
         row[tok] = [round(m, 2) for m in ms]
