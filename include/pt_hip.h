@@ -258,11 +258,11 @@ PT_API int pt_set_rise_repair(pt_context *ctx, int enabled);
  * count of the finished samples, the state, and the path in flight; the next pt_render with the same
  * camera, scene, textures, sky and RNG state starts every pixel from there.  Any other next launch ignores the stash: the stored RNG
  * state and accumulation are always those of the calls made, so results are the reference's either
- * way.  Once the tile queue of a launch is empty, a wave goes back to the tiles it finished and
- * continues their run-ahead until every tile of the launch is done (tail fill).
+ * way.  Run-ahead lanes piggyback on the lanes with samples of the launch left (they walk and shade
+ * only in rounds where such a lane does the same), so they never lengthen a tile.
  * 0 = automatic (the default; stops while the camera or scene changes at every launch),
- * 1 = off, 2 = make a stash at every launch (tests), 3 = automatic without the tail fill (A/B),
- * 4 = make stashes but never use them (diagnostic: the cost of the run-ahead work alone). */
+ * 1 = off, 2 = make a stash at every launch (tests), 3 = make stashes but never use them
+ * (diagnostic: the cost of the run-ahead work alone). */
 PT_API int pt_set_run_ahead(pt_context *ctx, int mode);
 /* Tuning knob of the cold start (the first launch after a scene, texture or camera change, which has
  * no tile costs yet).  prepass_spp = 0 (default): a launch of several render() calls runs its first

@@ -324,7 +324,8 @@ class Pathtracer:
 
     def set_run_ahead(self, mode: int) -> None:
         """Run-ahead across render() calls (pt_set_run_ahead): 0 automatic, 1 off, 2 always make a
-        stash, 3 automatic without the tail fill.  Results are the reference's for every setting."""
+        stash, 3 make stashes but never use them (diagnostic).  Results are the reference's for every
+        setting."""
         for c in self._contexts():
             N.check_ctx(N.hip().pt_set_run_ahead(c, int(mode)), c)
 

@@ -116,8 +116,6 @@ struct TraceParams {
     uint32_t* ahead;
     uint32_t aheadUse;          // != 0: the stash was made under this launch's camera and scene: consume it
     uint32_t aheadMake;         // != 0: lanes whose pixel is done go on with the next call's samples
-    uint32_t aheadTail;         // != 0 (persistent grids): once the tile queue is empty, a wave goes back to
-                                // the tiles it finished and continues their run-ahead (tail fill)
 };
 
 // Speculative sample groups: window of a group's start offset in which an earlier group's parse can
@@ -800,9 +798,12 @@ struct TravState {
 // The interior walk is walk_interior (the lean form: wave-uniform slab-form choice, unconditional
 // far-child write).  WW = 200 + EXITQ selects this traversal.  NOREPAIR (a test-only instantiation,
 // pt_set_rise_repair) skips repair_pending: the negative control that shows a scene exercises it.
-template <bool STATS, int EXITQ, bool NOREPAIR = false>
+// PIGGY (run-ahead launches): lanes with `second` set (run-ahead lanes) do not keep the wave in the
+// walk -- it also leaves as soon as no other lane is walking.
+template <bool STATS, int EXITQ, bool NOREPAIR = false, bool PIGGY = false>
 PT_DEV bool traverse_cb_phase(const float4* __restrict__ cnodes, const float4* __restrict__ prims, uint2* stack,
-                              const TraceParams& P, f3 o, f3 d, bool fresh, TravState& ts, Counters& cnt)
+                              const TraceParams& P, f3 o, f3 d, bool fresh, TravState& ts, Counters& cnt,
+                              bool second = false)
 {
     const float tMin = 0.001f;
     SlabRay R;
@@ -873,6 +874,7 @@ PT_DEV bool traverse_cb_phase(const float4* __restrict__ cnodes, const float4* _
         if (!pop()) { done = true; break; }
         // early exit once at most EXITQ/64 of the lanes that entered are still walking
         if ((uint32_t)__popcll(__ballot(1)) * 64u <= nAct * (uint32_t)EXITQ) break;
+        if (PIGGY && __ballot(!second) == 0ull) break;
     }
     ts.sp = sp;
     ts.cur = cur;
@@ -1267,42 +1269,6 @@ PT_DEV void ahead_save(const TraceParams& P, const PixelCtx& pc, const Xorwow& r
     A[22 * n + li] = ps.bounce;
 }
 
-// Tail fill (MODE 4, persistent): a wave whose tile queue is empty goes back to a tile it finished in
-// this launch and resumes its lanes' run-ahead from the stash they left (ahead_save, written by this
-// wave: program order, no other CU involved).  Lanes that finished a whole next call stay done.
-PT_DEV void ahead_resume(const TraceParams& P, const PixelCtx& pc, Xorwow& rng, PathState& ps)
-{
-    const uint32_t* A = P.ahead;
-    const size_t n = pc.npix, li = pc.li;
-    const uint32_t w = A[3 * n + li];
-    ps.c = P.chunks;
-    ps.alive = (w >> 31) != 0u;                  // a path in flight (a lane with w == 0 has no stash)
-    ps.s = w & 0x7fffffffu;
-    ps.color = mk(__uint_as_float(A[li]), __uint_as_float(A[n + li]), __uint_as_float(A[2 * n + li]));
-    rng.d = A[4 * n + li];
-    rng.v0 = A[5 * n + li];
-    rng.v1 = A[6 * n + li];
-    rng.v2 = A[7 * n + li];
-    rng.v3 = A[8 * n + li];
-    rng.v4 = A[9 * n + li];
-    if (!ps.alive) return;
-    ps.o = mk(__uint_as_float(A[10 * n + li]), __uint_as_float(A[11 * n + li]), __uint_as_float(A[12 * n + li]));
-    ps.d = mk(__uint_as_float(A[13 * n + li]), __uint_as_float(A[14 * n + li]), __uint_as_float(A[15 * n + li]));
-    ps.L = mk(__uint_as_float(A[16 * n + li]), __uint_as_float(A[17 * n + li]), __uint_as_float(A[18 * n + li]));
-    ps.T = mk(__uint_as_float(A[19 * n + li]), __uint_as_float(A[20 * n + li]), __uint_as_float(A[21 * n + li]));
-    ps.bounce = A[22 * n + li];
-}
-
-// Every tile of the launch has finished its samples of this launch (tail fill stops): the tiles
-// finished so far, counted in the persistent cursor's third word.
-PT_DEV bool ahead_all_done(const TraceParams& P)
-{
-    // an atomic RMW, not a load: a plain (even atomic) load may be served by this XCD's L2 copy
-    const uint32_t lane = threadIdx.x & 63u;
-    uint32_t d = 0;
-    if (lane == (uint32_t)(__ffsll((long long)__ballot(1)) - 1)) d = atomicAdd(P.tileCursor + 2, 0u);
-    return __builtin_amdgcn_readfirstlane(__builtin_amdgcn_readlane(d, __ffsll((long long)__ballot(1)) - 1)) >= P.numSlots;
-}
 
 PT_DEV void store_pixel(const TraceParams& P, const PixelCtx& pc, const Xorwow& rng, const PathState& ps)
 {
@@ -1654,21 +1620,8 @@ __global__ void __launch_bounds__(WPB * 64, MINW) trace_kernel(TraceParams P)
     const uint32_t accL = 4u * sceneF4 + WPB * stackWords + wave * 192u + lane;   // float index
     Counters cnt = {};
     uint32_t slot = PERSIST ? wave_fetch(P.tileCursor, 1u) : __builtin_amdgcn_readfirstlane(blockIdx.x * (uint32_t)WPB + wave);
-    // MODE 4 tail fill: the positions this wave finished, lane k holding the k-th (mod 64)
-    uint32_t doneList = 0, nDone = 0;
     for (;;) {
-    bool tailTile = false;                        // MODE 4: a finished tile revisited for its run-ahead
-    if (slot >= P.numSlots) {                     // also the grid's spare slots past the last item
-        if constexpr (AHEAD && PERSIST) {
-            if (!P.aheadTail || !P.aheadMake || nDone == 0 || ahead_all_done(P)) break;
-            --nDone;
-            slot = __builtin_amdgcn_readlane(doneList, __builtin_amdgcn_readfirstlane(nDone) & 63u);
-            tailTile = true;
-            if (nDone == 0 || (nDone & 63u) == 0u) nDone = 0;   // older entries were overwritten
-        } else {
-            break;
-        }
-    }
+    if (slot >= P.numSlots) break;               // also the grid's spare slots past the last item
     uint32_t tile, grp = 0, pos = slot;              // pos: the tile's position in the order
     if (SSG && !P.ssgPatch) {
         const uint32_t J = 2 * P.ssgG - 1;
@@ -1681,8 +1634,7 @@ __global__ void __launch_bounds__(WPB * 64, MINW) trace_kernel(TraceParams P)
     // end the launch.  Waves on the head of the order take issue slots first (s_setprio), the rest
     // fill the gaps.  pos is wave-uniform (an SGPR), so only one s_setprio executes.  Scheduling
     // only: results are identical.
-    if (tailTile) __builtin_amdgcn_s_setprio(0);
-    else if (pos < P.prio[0]) __builtin_amdgcn_s_setprio(3);
+    if (pos < P.prio[0]) __builtin_amdgcn_s_setprio(3);
     else if (pos < P.prio[1]) __builtin_amdgcn_s_setprio(2);
     else if (pos < P.prio[2]) __builtin_amdgcn_s_setprio(1);
     else __builtin_amdgcn_s_setprio(0);
@@ -1695,13 +1647,8 @@ __global__ void __launch_bounds__(WPB * 64, MINW) trace_kernel(TraceParams P)
         SsgLane sl;
         bool inFlight = false;
         if (SSG) ssg_load(P, pos, grp, lane, pc.li, pc.npix, rng, ps, sl);
-        else if (AHEAD && tailTile) {
-            ps.acc = accL;
-            __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "workgroup");   // this wave's own stash stores first
-            ahead_resume(P, pc, rng, ps);
-            inFlight = true;                      // (a lane without a path in flight is not alive)
-        } else load_pixel<AUX>(P, pc, rng, ps, accL);
-        if (AHEAD && P.aheadUse && !tailTile) {
+        else load_pixel<AUX>(P, pc, rng, ps, accL);
+        if (AHEAD && P.aheadUse) {
             inFlight = ahead_load(P, pc, rng, ps);
             if (ps.s == P.spp) end_call<true>(P, pc, ps, rng);     // a whole call was stashed
         }
@@ -1724,23 +1671,37 @@ __global__ void __launch_bounds__(WPB * 64, MINW) trace_kernel(TraceParams P)
             bool fresh = true, held = false;
             TravState ts = {0u, 0u, 0xffffffffu, kFltMax};
             while (ps.alive) {
-                // only run-ahead lanes left (a revisited tile: until every tile's own samples are done)
-                if (AHEAD && (tailTile ? ahead_all_done(P) : __ballot(ps.c < P.chunks) == 0ull)) break;
+                if (AHEAD && __ballot(ps.c < P.chunks) == 0ull) break;   // only run-ahead lanes left
                 if (STATS && fresh && !held) { cnt.segments++; wave_tick(cnt.w_segments); }
                 bool tdone = true;
+                // AHEAD: run-ahead lanes piggyback on the lanes with samples of this launch left ("main"
+                // lanes): they walk only in rounds where a main lane walks, shade a class (hit / miss)
+                // only in rounds where a main lane shades it, and never hold a main lane back -- the
+                // wave runs no code path for run-ahead lanes alone, so they do not lengthen the tile
+                const bool second = AHEAD && ps.c == P.chunks;
                 if (!held) {
-                    tdone = traverse_cb_phase<STATS, WW % 100, NOREPAIR>(nodes, prims, reinterpret_cast<uint2*>(stack), P,
-                                                                ps.o, ps.d, fresh, ts, cnt);
-                    fresh = tdone;
+                    if (AHEAD && second && __ballot(!second) == 0ull) {
+                        tdone = false;                             // no main lane walks this round
+                    } else {
+                        tdone = traverse_cb_phase<STATS, WW % 100, NOREPAIR, AHEAD>(
+                            nodes, prims, reinterpret_cast<uint2*>(stack), P, ps.o, ps.d, fresh, ts, cnt, second);
+                        fresh = tdone;
+                    }
                 }
                 if (DEFERQ > 0 || SKYQ > 0) {
                     const bool hitReady = tdone && ts.elem != 0xffffffffu;
                     const bool missReady = tdone && ts.elem == 0xffffffffu;
-                    const uint32_t na = (uint32_t)__popcll(__ballot(1));
+                    // (main lanes decide among themselves; run-ahead lanes never make them wait)
+                    const uint32_t na = (uint32_t)__popcll(__ballot(!second));
                     bool hold = false;
-                    if (DEFERQ > 0) hold = hitReady && (uint32_t)__popcll(__ballot(hitReady)) * 8u < na * (uint32_t)DEFERQ;
+                    if (DEFERQ > 0) hold = hitReady && (uint32_t)__popcll(__ballot(hitReady && !second)) * 8u < na * (uint32_t)DEFERQ;
                     if (SKYQ > 0 && P.skybox != 0)     // without a sky texture a miss costs next to nothing
-                        hold = hold || (missReady && (uint32_t)__popcll(__ballot(missReady)) * 8u < na * (uint32_t)SKYQ);
+                        hold = hold || (missReady && (uint32_t)__popcll(__ballot(missReady && !second)) * 8u < na * (uint32_t)SKYQ);
+                    if (AHEAD) {
+                        const bool mainHit = __ballot(hitReady && !second && !hold) != 0ull;
+                        const bool mainMiss = __ballot(missReady && !second && !hold) != 0ull;
+                        if (second) hold = (hitReady && !mainHit) || (missReady && !mainMiss);
+                    }
                     held = hold;
                     if (held) continue;
                 }
@@ -1801,13 +1762,7 @@ __global__ void __launch_bounds__(WPB * 64, MINW) trace_kernel(TraceParams P)
             P.pairsOut[pc.npix + pc.li] = -1.0f;      // odd-length fraction unknown
         }
     }
-    if (AHEAD && PERSIST && !tailTile) {
-        // tail fill: remember the tile, count it finished (the revisits stop when all are)
-        if (lane == (nDone & 63u)) doneList = pos;
-        ++nDone;
-        if (lane == 0) atomicAdd(P.tileCursor + 2, 1u);
-    }
-    if (P.tileCost && lane == 0 && (tile >> 16) < P.tilesY && !tailTile) {
+    if (P.tileCost && lane == 0 && (tile >> 16) < P.tilesY) {
         const uint32_t cyc = (uint32_t)min(__builtin_amdgcn_s_memtime() - tWave, (uint64_t)0xffffffffu);
         const uint32_t lin = (tile >> 16) * P.tilesX + (tile & 0xffffu);
         if (SSG) atomicAdd(&P.tileCost[lin], cyc / P.ssgG);   // zeroed before the launch (idle items add ~0)
@@ -1818,7 +1773,7 @@ __global__ void __launch_bounds__(WPB * 64, MINW) trace_kernel(TraceParams P)
             for (uint32_t k = 1; k < P.strip && (tile & 0xffffu) + k < P.tilesX; ++k) P.tileCost[lin + k] = 0u;
     }
     if (!PERSIST) break;
-    slot = tailTile ? P.numSlots : wave_fetch(P.tileCursor, 1u);
+    slot = wave_fetch(P.tileCursor, 1u);
     }
     if (PERSIST) {
         // the last wave to leave rewinds the cursor for the next launch (every wave has made its
@@ -1826,7 +1781,6 @@ __global__ void __launch_bounds__(WPB * 64, MINW) trace_kernel(TraceParams P)
         if (wave_fetch(P.tileCursor + 1, 1u) == gridDim.x * (uint32_t)WPB - 1 && lane == 0) {
             P.tileCursor[0] = 0;
             P.tileCursor[1] = 0;
-            P.tileCursor[2] = 0;
         }
     }
     flush_counters<STATS>(P, cnt);
@@ -2232,7 +2186,7 @@ struct pt_context {
     pt_camera aheadCam = {};
     uint64_t aheadState = 0;          // stateEpoch when it was made
     uint32_t aheadMisses = 0;         // consecutive launches that could not use the previous stash
-    int aheadMode = 0;                // pt_set_run_ahead: 0 automatic, 1 off, 2 always make a stash, 3 = 0 without tail fill
+    int aheadMode = 0;                // pt_set_run_ahead: 0 automatic, 1 off, 2 always make a stash, 3 make but never use
     uint32_t prepassSpp = 0;          // pt_set_cold_start: 0 = first call split off (pre-pass of kPrepassSpp for
                                       // one-call launches), > 0 = a discarded pre-pass of that many spp
     bool coldPriority = true;         // pt_set_cold_start: issue priority on the cold start's order
@@ -3205,7 +3159,7 @@ static int render_impl(pt_context* ctx, const pt_camera* cam, uint32_t spp, uint
     // (strip units or sample groups forced by their knobs take precedence over automatic run-ahead)
     const bool aheadCapable = !stats && !noRepair && ctx->cnodes && strip_capable(pick_variant(ctx)) && ctx->aheadMode != 1 &&
                               (ctx->aheadMode == 2 || (ctx->stripMode < 2 && ctx->ssgMode < 2));
-    const bool aheadUse = aheadCapable && stashMatches && ctx->aheadMode != 4;   // 4: diagnostic, never consume
+    const bool aheadUse = aheadCapable && stashMatches && ctx->aheadMode != 3;   // 3: diagnostic, never consume
     const bool aheadMake = aheadCapable && (ctx->aheadMode == 2 ||
         (launchSamples >= kAheadMinSamples && launchSamples <= kAheadMaxSamples && ctx->aheadMisses < 2));
     const bool ahead = aheadUse || aheadMake;
@@ -3233,8 +3187,8 @@ static int render_impl(pt_context* ctx, const pt_camera* cam, uint32_t spp, uint
     P.scatterWaves = ctx->schedule == 2 ? (uint32_t)(((size_t)ctx->rows * ctx->width + 63) / 64) : 0u;
     if (P.scatterWaves) P.order = nullptr;          // scattered mapping: slot = wave index
     if (!ctx->tileCursor) {
-        PT_HIP_CHECK(ctx, hipMalloc(&ctx->tileCursor, 4 * sizeof(uint32_t)));   // next slot, waves out, tiles done
-        PT_HIP_CHECK(ctx, hipMemset(ctx->tileCursor, 0, 4 * sizeof(uint32_t)));
+        PT_HIP_CHECK(ctx, hipMalloc(&ctx->tileCursor, 2 * sizeof(uint32_t)));
+        PT_HIP_CHECK(ctx, hipMemset(ctx->tileCursor, 0, 2 * sizeof(uint32_t)));
     }
     P.tileCursor = ctx->tileCursor;
     P.numSlots = units;
@@ -3268,7 +3222,6 @@ static int render_impl(pt_context* ctx, const pt_camera* cam, uint32_t spp, uint
         P.ahead = ctx->ahead;
         P.aheadUse = aheadUse ? 1u : 0u;
         P.aheadMake = aheadMake ? 1u : 0u;
-        P.aheadTail = (ctx->aheadMode == 3 || ctx->aheadMode == 4) ? 0u : 1u;
     }
     if (noRepair) {
         if (variant != 40 || stats)
@@ -3425,7 +3378,7 @@ PT_API int pt_set_cold_start(pt_context* ctx, uint32_t prepass_spp, int priority
 
 PT_API int pt_set_run_ahead(pt_context* ctx, int mode)
 {
-    if (!ctx || mode < 0 || mode > 4) return PT_ERR_ARG;
+    if (!ctx || mode < 0 || mode > 3) return PT_ERR_ARG;
     ctx->aheadMode = mode;
     return PT_OK;
 }

@@ -862,8 +862,8 @@ def test_run_ahead_call_loop_bitexact_vs_oracle(gpu_available, scenes, W, H):
 
 
 def test_run_ahead_modes_same_bits_full_frame(gpu_available, scenes):
-    # the whole 1080p frame, 24 calls of 8 spp: run-ahead automatic (with the tail fill), off, always,
-    # automatic without the tail fill -- identical accumulation and RNG state; the fused launch agrees
+    # the whole 1080p frame, 24 calls of 8 spp: run-ahead automatic, off, always, made but never used
+    # -- identical accumulation and RNG state; the fused launch agrees
     W, H = 1920, 1080
     pt = pa.Pathtracer(W, H)
     cam = pt.load_scene(scenes / "generated_scene.scene.json")

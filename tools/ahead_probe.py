@@ -1,7 +1,7 @@
 """Per-call GPU times of the reference's call loop (render(cam, 8, i == 0) per call) under run-ahead
-modes (pt_set_run_ahead: 1 off, 3 automatic without tail fill, 4 make-but-never-use, 0 automatic),
+modes (pt_set_run_ahead: 1 off, 3 make-but-never-use, 0 automatic),
 interleaved rounds in one process; results cross-checked bit-identical.
-    python tools/ahead_probe.py [--calls 32] [--modes 1,3,4,0] [--rounds 3]
+    python tools/ahead_probe.py [--calls 32] [--modes 1,3,0] [--rounds 3]
 """
 import argparse
 import json
@@ -20,7 +20,7 @@ ap.add_argument("--width", type=int, default=1920)
 ap.add_argument("--height", type=int, default=1080)
 ap.add_argument("--calls", type=int, default=32)
 ap.add_argument("--call-spp", type=int, default=8)
-ap.add_argument("--modes", default="1,3,4,0")
+ap.add_argument("--modes", default="1,3,0")
 ap.add_argument("--rounds", type=int, default=3)
 a = ap.parse_args()
 pt = pa.Pathtracer(a.width, a.height)
