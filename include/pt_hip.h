@@ -254,12 +254,11 @@ PT_API int pt_set_strip_units(pt_context *ctx, int mode);
 PT_API int pt_set_rise_repair(pt_context *ctx, int enabled);
 /* Run-ahead across render() calls: a launch of 3..64 samples per pixel (the reference's
  * render(camera, 8, ...) calls, main.cpp:272-279) lets the lanes whose pixels are done go on with the
- * pixel's next call (same XORWOW stream) until their tile ends, and keeps per pixel the colour sum and
- * count of the finished samples, the state, and the path in flight; the next pt_render with the same
- * camera, scene, textures, sky and RNG state starts every pixel from there.  Any other next launch ignores the stash: the stored RNG
- * state and accumulation are always those of the calls made, so results are the reference's either
- * way.  Run-ahead lanes piggyback on the lanes with samples of the launch left (they walk and shade
- * only in rounds where such a lane does the same), so they never lengthen a tile.
+ * pixel's next call (same XORWOW stream) until their tile ends, and keeps per pixel the colour sum,
+ * count and state after the last finished sample; the next pt_render with the same camera, scene,
+ * textures, sky and RNG state starts every pixel from there.  Any other next launch ignores the
+ * stash: the stored RNG state and accumulation are always those of the calls made, so results are
+ * the reference's either way.
  * 0 = automatic (the default; stops while the camera or scene changes at every launch),
  * 1 = off, 2 = make a stash at every launch (tests), 3 = make stashes but never use them
  * (diagnostic: the cost of the run-ahead work alone). */

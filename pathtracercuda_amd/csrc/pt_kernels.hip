@@ -112,7 +112,7 @@ struct TraceParams {
     uint32_t prio[3];           // issue priority by order position: < prio[0] -> 3, < prio[1] -> 2, < prio[2] -> 1
     uint32_t strip;             // MODE 3: tiles per dispatch unit (a row strip of `strip` tiles; see trace_kernel)
     // MODE 4 (run-ahead across render() calls, see trace_kernel): per-pixel stash of the NEXT call's
-    // progress, kAheadWords planes of rows x width u32 (ahead_save).
+    // first samples, kAheadWords planes of rows x width u32 (ahead_store).
     uint32_t* ahead;
     uint32_t aheadUse;          // != 0: the stash was made under this launch's camera and scene: consume it
     uint32_t aheadMake;         // != 0: lanes whose pixel is done go on with the next call's samples
@@ -131,9 +131,7 @@ static inline uint32_t ssg_window_words(uint32_t G, uint32_t n)
 constexpr uint32_t kFoldBatch = 16;       // samples the fold loads at once
 constexpr uint32_t kStatWords = 23;       // counters of an instrumented launch (pt_render_stats)
 constexpr uint32_t kStartWords = 8;       // start record: offset, d, v0..v4, stop offset (last group)
-// run-ahead stash (ahead_save): colour sum x3, samples | in-flight << 31, XORWOW state x6, and the
-// in-flight path -- ray origin x3, direction x3, radiance x3, throughput x3, bounce
-constexpr uint32_t kAheadWords = 23;
+constexpr uint32_t kAheadWords = 10;      // run-ahead stash: colour sum x3, samples, XORWOW state x6
 enum : uint32_t { F_ACC = 0, F_COL = 3, F_SC = 6, F_DONE = 7, F_OFF = 8, F_H = 9, F_ST = 10, F_FLAG = 16, F_ODD = 17,
                   F_SQ = 18, kFoldWords = 19 };
 
@@ -798,12 +796,9 @@ struct TravState {
 // The interior walk is walk_interior (the lean form: wave-uniform slab-form choice, unconditional
 // far-child write).  WW = 200 + EXITQ selects this traversal.  NOREPAIR (a test-only instantiation,
 // pt_set_rise_repair) skips repair_pending: the negative control that shows a scene exercises it.
-// PIGGY (run-ahead launches): lanes with `second` set (run-ahead lanes) do not keep the wave in the
-// walk -- it also leaves as soon as no other lane is walking.
-template <bool STATS, int EXITQ, bool NOREPAIR = false, bool PIGGY = false>
+template <bool STATS, int EXITQ, bool NOREPAIR = false>
 PT_DEV bool traverse_cb_phase(const float4* __restrict__ cnodes, const float4* __restrict__ prims, uint2* stack,
-                              const TraceParams& P, f3 o, f3 d, bool fresh, TravState& ts, Counters& cnt,
-                              bool second = false)
+                              const TraceParams& P, f3 o, f3 d, bool fresh, TravState& ts, Counters& cnt)
 {
     const float tMin = 0.001f;
     SlabRay R;
@@ -874,7 +869,6 @@ PT_DEV bool traverse_cb_phase(const float4* __restrict__ cnodes, const float4* _
         if (!pop()) { done = true; break; }
         // early exit once at most EXITQ/64 of the lanes that entered are still walking
         if ((uint32_t)__popcll(__ballot(1)) * 64u <= nAct * (uint32_t)EXITQ) break;
-        if (PIGGY && __ballot(!second) == 0ull) break;
     }
     ts.sp = sp;
     ts.cur = cur;
@@ -1202,19 +1196,15 @@ PT_DEV void load_pixel(const TraceParams& P, const PixelCtx& pc, Xorwow& rng, Pa
     }
 }
 
-// Run-ahead (MODE 4): the previous launch's progress on this call (same camera, scene, textures, sky
-// and RNG state: the host checked the key) -- k finished samples summed in order, and the path of
-// sample k in flight (its ray, radiance, throughput, bounce and the stream's state at that point).
-// Usable when the samples fit in this call: k < spp, or k == spp with no path in flight.  Returns
-// true when a path in flight was restored (the caller then skips the camera ray).
-PT_DEV bool ahead_load(const TraceParams& P, const PixelCtx& pc, Xorwow& rng, PathState& ps)
+// Run-ahead (MODE 4): the previous launch's stash of this call's first k samples (same camera, scene,
+// textures, sky and RNG state: the host checked the key) -- their colour sum in sample order from 0
+// and the XORWOW state after them.  A stash longer than this call's spp cannot be split: dropped.
+PT_DEV void ahead_load(const TraceParams& P, const PixelCtx& pc, Xorwow& rng, PathState& ps)
 {
     const uint32_t* A = P.ahead;
     const size_t n = pc.npix, li = pc.li;
-    const uint32_t w = A[3 * n + li];
-    const uint32_t k = w & 0x7fffffffu;
-    const bool inFlight = (w >> 31) != 0u;
-    if (w == 0u || k > P.spp || (k == P.spp && inFlight)) return false;
+    const uint32_t k = A[3 * n + li];
+    if (k == 0u || k > P.spp) return;
     ps.color = mk(__uint_as_float(A[li]), __uint_as_float(A[n + li]), __uint_as_float(A[2 * n + li]));
     ps.s = k;
     rng.d = A[4 * n + li];
@@ -1223,52 +1213,7 @@ PT_DEV bool ahead_load(const TraceParams& P, const PixelCtx& pc, Xorwow& rng, Pa
     rng.v2 = A[7 * n + li];
     rng.v3 = A[8 * n + li];
     rng.v4 = A[9 * n + li];
-    if (!inFlight) return false;
-    ps.o = mk(__uint_as_float(A[10 * n + li]), __uint_as_float(A[11 * n + li]), __uint_as_float(A[12 * n + li]));
-    ps.d = mk(__uint_as_float(A[13 * n + li]), __uint_as_float(A[14 * n + li]), __uint_as_float(A[15 * n + li]));
-    ps.L = mk(__uint_as_float(A[16 * n + li]), __uint_as_float(A[17 * n + li]), __uint_as_float(A[18 * n + li]));
-    ps.T = mk(__uint_as_float(A[19 * n + li]), __uint_as_float(A[20 * n + li]), __uint_as_float(A[21 * n + li]));
-    ps.bounce = A[22 * n + li];
-    return true;
 }
-
-// The stash a lane leaves when its tile ends (MODE 4 with aheadMake): the next call's samples it has
-// finished and, if it is still alive, the path it is tracing -- at the top of the segment loop, so the
-// path's next ray (origin, direction), radiance, throughput, bounce and the stream's state are exactly
-// those with which the path continues; the next launch traces that ray afresh (the traversal of a
-// ray is deterministic) and goes on.  No sample is repeated or lost.
-PT_DEV void ahead_save(const TraceParams& P, const PixelCtx& pc, const Xorwow& rng, const PathState& ps)
-{
-    uint32_t li = (uint32_t)pc.li;
-    asm volatile("" : "+v"(li));                 // addresses from one register (store_pixel)
-    uint32_t* A = P.ahead;
-    const size_t n = pc.npix;
-    A[li] = __float_as_uint(ps.color.x);
-    A[n + li] = __float_as_uint(ps.color.y);
-    A[2 * n + li] = __float_as_uint(ps.color.z);
-    A[3 * n + li] = ps.s | (ps.alive ? 0x80000000u : 0u);
-    A[4 * n + li] = rng.d;
-    A[5 * n + li] = rng.v0;
-    A[6 * n + li] = rng.v1;
-    A[7 * n + li] = rng.v2;
-    A[8 * n + li] = rng.v3;
-    A[9 * n + li] = rng.v4;
-    if (!ps.alive) return;
-    A[10 * n + li] = __float_as_uint(ps.o.x);
-    A[11 * n + li] = __float_as_uint(ps.o.y);
-    A[12 * n + li] = __float_as_uint(ps.o.z);
-    A[13 * n + li] = __float_as_uint(ps.d.x);
-    A[14 * n + li] = __float_as_uint(ps.d.y);
-    A[15 * n + li] = __float_as_uint(ps.d.z);
-    A[16 * n + li] = __float_as_uint(ps.L.x);
-    A[17 * n + li] = __float_as_uint(ps.L.y);
-    A[18 * n + li] = __float_as_uint(ps.L.z);
-    A[19 * n + li] = __float_as_uint(ps.T.x);
-    A[20 * n + li] = __float_as_uint(ps.T.y);
-    A[21 * n + li] = __float_as_uint(ps.T.z);
-    A[22 * n + li] = ps.bounce;
-}
-
 
 PT_DEV void store_pixel(const TraceParams& P, const PixelCtx& pc, const Xorwow& rng, const PathState& ps)
 {
@@ -1287,20 +1232,42 @@ PT_DEV void store_pixel(const TraceParams& P, const PixelCtx& pc, const Xorwow& 
     P.accum[li] = make_float4(a[0], a[64], a[128], 1.0f);   // trace.cu:198, once per launch
 }
 
+// Run-ahead (MODE 4): after every sample of the NEXT call a lane stashes the call's colour sum so far
+// (in sample order from 0), the sample count and the XORWOW state -- the state at a sample start, from
+// which the next launch continues (a sample in progress when the tile ends is redone there, from a
+// fresh camera ray like its neighbours').
+PT_DEV void ahead_store(const TraceParams& P, const PixelCtx& pc, const f3& color, uint32_t k, const Xorwow& rng)
+{
+    uint32_t li = (uint32_t)pc.li;
+    asm volatile("" : "+v"(li));                 // addresses from one register (store_pixel)
+    uint32_t* A = P.ahead;
+    const size_t n = pc.npix;
+    A[li] = __float_as_uint(color.x);
+    A[n + li] = __float_as_uint(color.y);
+    A[2 * n + li] = __float_as_uint(color.z);
+    A[3 * n + li] = k;
+    A[4 * n + li] = rng.d;
+    A[5 * n + li] = rng.v0;
+    A[6 * n + li] = rng.v1;
+    A[7 * n + li] = rng.v2;
+    A[8 * n + li] = rng.v3;
+    A[9 * n + li] = rng.v4;
+}
+
 // End of a path: sum it into the render() call's color; at the end of a call fold the call into
 // the accumulation value (trace.cu:193-198); start the next sample while any remain.  The running
 // accumulation value lives in the wave's LDS slice for the whole launch (loaded by load_pixel,
 // stored once by store_pixel), so a launch of many render() calls writes each pixel once instead of
 // once per call -- the fold and its order (color + accum) are unchanged.
 // The end of a render() call's samples (ps.s == spp): fold the call into the accumulation value
-// (trace.cu:193-198).  AHEAD: a lane already in run-ahead (ps.c == chunks) has done a whole next call
-// and stops (its sum and state are stashed when the tile ends, ahead_save); a lane finishing its last
-// call stores its pixel now (the call's RNG state and accumulation are final here) and, when the
-// launch makes a stash, goes on with the next call.
+// (trace.cu:193-198).  AHEAD: a lane already in run-ahead (ps.c == chunks) has done a whole next call:
+// it stashes it and stops; a lane finishing its last call stores its pixel now (the call's RNG state
+// and accumulation are final here) and, when the launch makes a stash, goes on with the next call.
 template <bool AHEAD>
 PT_DEV void end_call(const TraceParams& P, const PixelCtx& pc, PathState& ps, const Xorwow& rng)
 {
     if (AHEAD && ps.c == P.chunks) {
+        ahead_store(P, pc, ps.color, ps.s, rng);
         ps.alive = false;
         return;
     }
@@ -1317,6 +1284,7 @@ PT_DEV void end_call(const TraceParams& P, const PixelCtx& pc, PathState& ps, co
         ps.alive = false;
         if (AHEAD) {
             store_pixel(P, pc, rng, ps);
+            if (P.aheadMake) P.ahead[3 * pc.npix + (uint32_t)pc.li] = 0u;   // no stash until a next-call sample ends
             ps.alive = P.aheadMake != 0;
         }
     }
@@ -1329,6 +1297,7 @@ PT_DEV void finish_path(const TraceParams& P, PathState& ps, Xorwow& rng, float 
     ps.color = add(ps.color, ps.L);
     if (STATS) cnt.samples++;
     if (++ps.s == P.spp) end_call<AHEAD>(P, pc, ps, rng);
+    else if (AHEAD && ps.c == P.chunks) ahead_store(P, pc, ps.color, ps.s, rng);   // a next-call sample
     if (ps.alive) {
         camera_ray(P, fx, fy, rng, ps.o, ps.d);
         ps.L = splat(0.0f);
@@ -1592,11 +1561,11 @@ __global__ void __launch_bounds__(WPB * 64, MINW) trace_kernel(TraceParams P)
     // tile when its slowest pixel has finished; the lanes whose pixels finished first would idle until
     // then (28 % of lane time at 8 spp per call).  Here a lane whose pixel has finished
     // its last call stores the pixel (the call's final RNG state and accumulation value) and goes on
-    // with the pixel's NEXT call -- the same XORWOW stream -- until a whole next call is done or the
-    // tile ends: a wave leaves the tile as soon as no lane has samples of this launch left, and each
-    // lane then stashes its progress, the path in flight included (ahead_save).  The next launch
-    // continues from the stash when its camera and scene are the ones it was made with (host key,
-    // render_impl); otherwise the stored state is the exact one to continue from.
+    // with the pixel's NEXT call -- the same XORWOW stream -- stashing after every sample the colour
+    // sum so far, the sample count and the state (ahead_store), until the tile ends or a whole next
+    // call is done.  A wave leaves the tile as soon as no lane has samples of this launch left.  The
+    // next launch continues from the stash when its camera and scene are the ones it was made with
+    // (host key, render_impl); otherwise the stored state is the exact one to continue from.
     constexpr bool SSG = MODE == 1, AUX = MODE == 2, STRIP = MODE == 3, AHEAD = MODE == 4;
     const uint32_t lane = threadIdx.x & 63u;
     const uint32_t wave = threadIdx.x >> 6;
@@ -1645,15 +1614,14 @@ __global__ void __launch_bounds__(WPB * 64, MINW) trace_kernel(TraceParams P)
         Xorwow rng;
         PathState ps;
         SsgLane sl;
-        bool inFlight = false;
         if (SSG) ssg_load(P, pos, grp, lane, pc.li, pc.npix, rng, ps, sl);
         else load_pixel<AUX>(P, pc, rng, ps, accL);
         if (AHEAD && P.aheadUse) {
-            inFlight = ahead_load(P, pc, rng, ps);
+            ahead_load(P, pc, rng, ps);
             if (ps.s == P.spp) end_call<true>(P, pc, ps, rng);     // a whole call was stashed
         }
         float fx = (float)(int32_t)pc.px, fy = (float)(int32_t)pc.py;
-        if (!inFlight) camera_ray(P, fx, fy, rng, ps.o, ps.d);
+        camera_ray(P, fx, fy, rng, ps.o, ps.d);
         uint32_t stripK = 0;                     // STRIP: this lane's tile within the unit
         uint64_t tAll = STATS ? __builtin_amdgcn_s_memtime() : 0;
         uint64_t tDone = 0;
@@ -1674,34 +1642,19 @@ __global__ void __launch_bounds__(WPB * 64, MINW) trace_kernel(TraceParams P)
                 if (AHEAD && __ballot(ps.c < P.chunks) == 0ull) break;   // only run-ahead lanes left
                 if (STATS && fresh && !held) { cnt.segments++; wave_tick(cnt.w_segments); }
                 bool tdone = true;
-                // AHEAD: run-ahead lanes piggyback on the lanes with samples of this launch left ("main"
-                // lanes): they walk only in rounds where a main lane walks, shade a class (hit / miss)
-                // only in rounds where a main lane shades it, and never hold a main lane back -- the
-                // wave runs no code path for run-ahead lanes alone, so they do not lengthen the tile
-                const bool second = AHEAD && ps.c == P.chunks;
                 if (!held) {
-                    if (AHEAD && second && __ballot(!second) == 0ull) {
-                        tdone = false;                             // no main lane walks this round
-                    } else {
-                        tdone = traverse_cb_phase<STATS, WW % 100, NOREPAIR, AHEAD>(
-                            nodes, prims, reinterpret_cast<uint2*>(stack), P, ps.o, ps.d, fresh, ts, cnt, second);
-                        fresh = tdone;
-                    }
+                    tdone = traverse_cb_phase<STATS, WW % 100, NOREPAIR>(nodes, prims, reinterpret_cast<uint2*>(stack), P,
+                                                                ps.o, ps.d, fresh, ts, cnt);
+                    fresh = tdone;
                 }
                 if (DEFERQ > 0 || SKYQ > 0) {
                     const bool hitReady = tdone && ts.elem != 0xffffffffu;
                     const bool missReady = tdone && ts.elem == 0xffffffffu;
-                    // (main lanes decide among themselves; run-ahead lanes never make them wait)
-                    const uint32_t na = (uint32_t)__popcll(__ballot(!second));
+                    const uint32_t na = (uint32_t)__popcll(__ballot(1));
                     bool hold = false;
-                    if (DEFERQ > 0) hold = hitReady && (uint32_t)__popcll(__ballot(hitReady && !second)) * 8u < na * (uint32_t)DEFERQ;
+                    if (DEFERQ > 0) hold = hitReady && (uint32_t)__popcll(__ballot(hitReady)) * 8u < na * (uint32_t)DEFERQ;
                     if (SKYQ > 0 && P.skybox != 0)     // without a sky texture a miss costs next to nothing
-                        hold = hold || (missReady && (uint32_t)__popcll(__ballot(missReady && !second)) * 8u < na * (uint32_t)SKYQ);
-                    if (AHEAD) {
-                        const bool mainHit = __ballot(hitReady && !second && !hold) != 0ull;
-                        const bool mainMiss = __ballot(missReady && !second && !hold) != 0ull;
-                        if (second) hold = (hitReady && !mainHit) || (missReady && !mainMiss);
-                    }
+                        hold = hold || (missReady && (uint32_t)__popcll(__ballot(missReady)) * 8u < na * (uint32_t)SKYQ);
                     held = hold;
                     if (held) continue;
                 }
@@ -1752,9 +1705,7 @@ __global__ void __launch_bounds__(WPB * 64, MINW) trace_kernel(TraceParams P)
         }
         if (STATS) wave_time(cnt.cyc_total, tAll);
         if (SSG) P.ssgCount[(size_t)sl.logItem * 64 + lane] = sl.k;
-        else if (AHEAD) {                     // the pixel was stored when its last call ended (end_call)
-            if (P.aheadMake) ahead_save(P, pc, rng, ps);
-        }
+        else if (AHEAD) {}                    // stored when its last call ended (end_call)
         else if (!P.discard) store_pixel(P, pc, rng, ps);
         else if (AUX && P.pairsOut)           // cost pre-pass: draw pairs per sample of this pixel
         {
