@@ -329,7 +329,18 @@ class Pathtracer:
         for c in self._contexts():
             N.check_ctx(N.hip().pt_set_run_ahead(c, int(mode)), c)
 
-    def set_cold_start(self, prepass_spp: int = 0, priority: bool = False) -> None:
+    def set_head_groups(self, tiles: int = 0, groups: int = 0) -> None:
+        """Head groups (pt_set_head_groups): 0 automatic, -1 off, K > 0 always the first K tiles of the
+        cost order as `groups`-way sample groups.  Results are identical for every setting."""
+        for c in self._contexts():
+            N.check_ctx(N.hip().pt_set_head_groups(c, int(tiles), int(groups)), c)
+
+    @property
+    def last_head_tiles(self) -> int:
+        """Head tiles of the last launch (a device group: the largest over its devices)."""
+        return max(int(N.hip().pt_last_head_tiles(c)) for c in self._contexts())
+
+    def set_cold_start(self, prepass_spp: int = 0, priority: bool = True) -> None:
         """Cold-start scheduling (pt_set_cold_start): cost pre-pass spp (0 = default) and issue
         priority on the pre-pass's order.  Results are identical for every setting."""
         for c in self._contexts():

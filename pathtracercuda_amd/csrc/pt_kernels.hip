@@ -116,6 +116,8 @@ struct TraceParams {
     uint32_t* ahead;
     uint32_t aheadUse;          // != 0: the stash was made under this launch's camera and scene: consume it
     uint32_t aheadMake;         // != 0: lanes whose pixel is done go on with the next call's samples
+    uint32_t headItems;         // MODE 5 (trace_head_kernel): slots below this are sample-group items of the
+                                // first ssgTiles tiles, the rest plain tiles from order position ssgTiles on
 };
 
 // Speculative sample groups: window of a group's start offset in which an earlier group's parse can
@@ -1546,16 +1548,50 @@ PT_DEV void ssg_finish(const TraceParams& P, PathState& ps, Xorwow& rng, float f
 // LDS layout per workgroup: [scene nodes (2 float4 each) | scene prims (4 float4 each)] when
 // SCENE_LDS, then WPB wave stacks of stackDepth x 64 u32.
 // ---------------------------------------------------------------------------------------------
-// SL = 0: scene read through the caches; 1: BVH nodes staged in LDS; 2: nodes and primitives in LDS.
-// One wave = one 8x8 tile.  PERSIST: the grid holds only the resident waves, and each wave takes
-// the next dispatch slot from a global counter when its tile is done, so a wave never waits for
-// the other waves of its workgroup (which would keep the group's LDS and slots idle).
-// MODE 0: plain; 1 (SSG): speculative sample groups (ssg_load / ssg_finish), one work item per
-// (tile, group); 2: auxiliary launches -- the resume pass after a grouped launch, and the cost
-// pre-pass that also measures draw pairs per sample.  Separate instantiations keep the plain
-// kernel's register allocation free of their code.
-template <bool STATS, int SL, int WPB, int WW, int MINW, bool PERSIST = false, int MODE = 0>
-__global__ void __launch_bounds__(WPB * 64, MINW) trace_kernel(TraceParams P)
+// The scene copied into the workgroup's LDS (SL >= 1), once per workgroup.
+template <int SL, int WPB, int WW>
+PT_DEV void stage_scene_impl(const TraceParams& P)
+{
+    if (SL < 1) return;
+    const float4* gnodes = WW >= 3 ? P.cnodes : P.nodes;
+    const uint32_t nodeF4 = WW >= 3 ? 4u * P.cnodeCount : 2u * P.nodeCount;
+    for (uint32_t i = threadIdx.x; i < nodeF4; i += WPB * 64) lds4[i] = gnodes[i];
+    if (SL >= 2)
+        for (uint32_t i = threadIdx.x; i < 4u * P.primCount; i += WPB * 64) lds4[nodeF4 + i] = P.prims[i];
+    __syncthreads();
+}
+
+// The LDS of a wave (trace_kernel's layout): the scene (SL >= 1: child-box records or nodes, SL >= 2:
+// primitives too), WPB wave stacks of stackDepth x 64 entries (u32 node index, or uint2 (word, lo) for
+// WW >= 3), then one accumulation slice per wave (3 planes of 64 floats).  Recomputed by every user
+// from threadIdx, so the pointers stay LDS pointers even in a non-inlined item function.
+template <int SL, int WPB, int WW>
+struct WaveLds {
+    const float4* nodes;
+    const float4* prims;
+    uint32_t* stack;
+    uint32_t accL;            // float index of this lane's accumulation value in the dynamic LDS
+};
+
+template <int SL, int WPB, int WW>
+PT_DEV WaveLds<SL, WPB, WW> wave_lds(const TraceParams& P)
+{
+    const uint32_t lane = threadIdx.x & 63u, wave = threadIdx.x >> 6;
+    const float4* gnodes = WW >= 3 ? P.cnodes : P.nodes;
+    const uint32_t nodeF4 = WW >= 3 ? 4u * P.cnodeCount : 2u * P.nodeCount;
+    const uint32_t sceneF4 = (SL >= 1 ? nodeF4 : 0u) + (SL >= 2 ? 4u * P.primCount : 0u);
+    WaveLds<SL, WPB, WW> L;
+    L.nodes = SL >= 1 ? lds4 : gnodes;
+    L.prims = SL >= 2 ? lds4 + nodeF4 : P.prims;
+    const uint32_t stackWords = (WW >= 3 ? 2u : 1u) * P.stackDepth * 64u;
+    L.stack = reinterpret_cast<uint32_t*>(lds4 + sceneF4) + wave * stackWords + (WW >= 3 ? 2u : 1u) * lane;
+    L.accL = 4u * sceneF4 + WPB * stackWords + wave * 192u + lane;
+    return L;
+}
+
+// One work item of trace_kernel: the tile at dispatch slot `slot` (MODE 1: the (tile, group) item).
+template <bool STATS, int SL, int WPB, int WW, int MINW, bool PERSIST, int MODE>
+PT_DEV void run_item(const TraceParams& P, uint32_t slot, Counters& cnt)
 {
     // MODE 4 (AHEAD): run-ahead across render() calls.  A launch of one or a few render() calls ends a
     // tile when its slowest pixel has finished; the lanes whose pixels finished first would idle until
@@ -1568,29 +1604,11 @@ __global__ void __launch_bounds__(WPB * 64, MINW) trace_kernel(TraceParams P)
     // (host key, render_impl); otherwise the stored state is the exact one to continue from.
     constexpr bool SSG = MODE == 1, AUX = MODE == 2, STRIP = MODE == 3, AHEAD = MODE == 4;
     const uint32_t lane = threadIdx.x & 63u;
-    const uint32_t wave = threadIdx.x >> 6;
-    const float4* gnodes = WW >= 3 ? P.cnodes : P.nodes;
-    const uint32_t nodeF4 = WW >= 3 ? 4u * P.cnodeCount : 2u * P.nodeCount;
-    const uint32_t stackDepth = P.stackDepth;
-    const uint32_t sceneF4 = (SL >= 1 ? nodeF4 : 0u) + (SL >= 2 ? 4u * P.primCount : 0u);
-    if (SL >= 1) {
-        for (uint32_t i = threadIdx.x; i < nodeF4; i += WPB * 64) lds4[i] = gnodes[i];
-        if (SL >= 2)
-            for (uint32_t i = threadIdx.x; i < 4u * P.primCount; i += WPB * 64) lds4[nodeF4 + i] = P.prims[i];
-        __syncthreads();
-    }
-    const float4* __restrict__ nodes = SL >= 1 ? lds4 : gnodes;
-    const float4* __restrict__ prims = SL >= 2 ? lds4 + nodeF4 : P.prims;
-    // wave stacks: stackDepth x 64 entries of u32 (node index), or of uint2 (word, lo) for WW >= 3;
-    // then one accumulation slice per wave (3 planes of 64 floats)
-    uint32_t* ldsStacks = reinterpret_cast<uint32_t*>(lds4 + sceneF4);
-    const uint32_t stackWords = (WW >= 3 ? 2u : 1u) * stackDepth * 64u;
-    uint32_t* stack = ldsStacks + wave * stackWords + (WW >= 3 ? 2u : 1u) * lane;
-    const uint32_t accL = 4u * sceneF4 + WPB * stackWords + wave * 192u + lane;   // float index
-    Counters cnt = {};
-    uint32_t slot = PERSIST ? wave_fetch(P.tileCursor, 1u) : __builtin_amdgcn_readfirstlane(blockIdx.x * (uint32_t)WPB + wave);
-    for (;;) {
-    if (slot >= P.numSlots) break;               // also the grid's spare slots past the last item
+    const WaveLds<SL, WPB, WW> Lw = wave_lds<SL, WPB, WW>(P);
+    const float4* __restrict__ nodes = Lw.nodes;
+    const float4* __restrict__ prims = Lw.prims;
+    uint32_t* stack = Lw.stack;
+    const uint32_t accL = Lw.accL;
     uint32_t tile, grp = 0, pos = slot;              // pos: the tile's position in the order
     if (SSG && !P.ssgPatch) {
         const uint32_t J = 2 * P.ssgG - 1;
@@ -1716,13 +1734,38 @@ __global__ void __launch_bounds__(WPB * 64, MINW) trace_kernel(TraceParams P)
     if (P.tileCost && lane == 0 && (tile >> 16) < P.tilesY) {
         const uint32_t cyc = (uint32_t)min(__builtin_amdgcn_s_memtime() - tWave, (uint64_t)0xffffffffu);
         const uint32_t lin = (tile >> 16) * P.tilesX + (tile & 0xffffu);
-        if (SSG) atomicAdd(&P.tileCost[lin], cyc / P.ssgG);   // zeroed before the launch (idle items add ~0)
+        // SSG: zeroed before the launch (idle items add ~0); in a head-group launch the head tiles rank
+        // among plain tiles, so they record their longest item x groups, close to a plain run's cycles
+        if (SSG && P.headItems) atomicMax(&P.tileCost[lin], (uint32_t)min((uint64_t)cyc * P.ssgG, (uint64_t)0xffffffffu));
+        else if (SSG) atomicAdd(&P.tileCost[lin], cyc / P.ssgG);
         else P.tileCost[lin] = cyc;
         // STRIP: the unit's cost sits at its first tile, the other tiles' entries are 0, so a sort of
         // the tile costs lists the units first (pt_render: the order of a strip launch)
         if (STRIP)
             for (uint32_t k = 1; k < P.strip && (tile & 0xffffu) + k < P.tilesX; ++k) P.tileCost[lin + k] = 0u;
     }
+}
+
+// SL = 0: scene read through the caches; 1: BVH nodes staged in LDS; 2: nodes and primitives in LDS.
+// One wave = one 8x8 tile.  PERSIST: the grid holds only the resident waves, and each wave takes
+// the next dispatch slot from a global counter when its tile is done, so a wave never waits for
+// the other waves of its workgroup (which would keep the group's LDS and slots idle).
+// MODE 0: plain; 1 (SSG): speculative sample groups (ssg_load / ssg_finish), one work item per
+// (tile, group); 2: auxiliary launches -- the resume pass after a grouped launch, and the cost
+// pre-pass that also measures draw pairs per sample; 3: strip units; 4: run-ahead across render()
+// calls (run_item).  Separate instantiations keep the plain kernel's register allocation free of
+// their code.
+template <bool STATS, int SL, int WPB, int WW, int MINW, bool PERSIST = false, int MODE = 0>
+__global__ void __launch_bounds__(WPB * 64, MINW) trace_kernel(TraceParams P)
+{
+    const uint32_t lane = threadIdx.x & 63u;
+    const uint32_t wave = threadIdx.x >> 6;
+    stage_scene_impl<SL, WPB, WW>(P);
+    Counters cnt = {};
+    uint32_t slot = PERSIST ? wave_fetch(P.tileCursor, 1u) : __builtin_amdgcn_readfirstlane(blockIdx.x * (uint32_t)WPB + wave);
+    for (;;) {
+    if (slot >= P.numSlots) break;               // also the grid's spare slots past the last item
+    run_item<STATS, SL, WPB, WW, MINW, PERSIST, MODE>(P, slot, cnt);
     if (!PERSIST) break;
     slot = wave_fetch(P.tileCursor, 1u);
     }
@@ -1735,6 +1778,49 @@ __global__ void __launch_bounds__(WPB * 64, MINW) trace_kernel(TraceParams P)
         }
     }
     flush_counters<STATS>(P, cnt);
+}
+
+
+// Head groups (MODE 5): one persistent queue holding the sample-group items of the
+// first `headTiles` tiles of the cost order (slots 0 .. headItems - 1, as a MODE 1 launch numbers
+// them) followed by the remaining tiles as plain tiles (MODE 0).  The two kinds of item run in
+// separate non-inlined functions, so each keeps the register allocation of its own instantiation
+// (a merged body spilled and slowed every tile); they read the launch parameters
+// through the kernel-argument pointer (scalar loads, as in the kernel).
+typedef const __attribute__((address_space(4))) TraceParams* KernargParams;
+
+template <int SL, int WPB, int WW, int MINW>
+__device__ __noinline__ void head_group_item(uint32_t slot)
+{
+    const TraceParams& P = *(const TraceParams*)(KernargParams)__builtin_amdgcn_kernarg_segment_ptr();
+    Counters cnt = {};
+    run_item<false, SL, WPB, WW, MINW, true, 1>(P, slot, cnt);
+}
+
+template <int SL, int WPB, int WW, int MINW>
+__device__ __noinline__ void head_plain_item(uint32_t slot)
+{
+    const TraceParams& P = *(const TraceParams*)(KernargParams)__builtin_amdgcn_kernarg_segment_ptr();
+    Counters cnt = {};
+    run_item<false, SL, WPB, WW, MINW, true, 0>(P, slot, cnt);
+}
+
+template <int SL, int WPB, int WW, int MINW>
+__global__ void __launch_bounds__(WPB * 64, MINW) trace_head_kernel(TraceParams P)
+{
+    const uint32_t wave = threadIdx.x >> 6;
+    stage_scene_impl<SL, WPB, WW>(P);
+    uint32_t slot = wave_fetch(P.tileCursor, 1u);
+    (void)wave;
+    while (slot < P.numSlots) {
+        if (slot < P.headItems) head_group_item<SL, WPB, WW, MINW>(slot);
+        else head_plain_item<SL, WPB, WW, MINW>(slot - P.headItems + P.ssgTiles);
+        slot = wave_fetch(P.tileCursor, 1u);
+    }
+    if (wave_fetch(P.tileCursor + 1, 1u) == gridDim.x * (uint32_t)WPB - 1 && (threadIdx.x & 63u) == 0) {
+        P.tileCursor[0] = 0;
+        P.tileCursor[1] = 0;
+    }
 }
 
 // initRandState (initRandState.cu:4-17): curand_init(1984 + x + y * width, 0, 0)
@@ -2143,6 +2229,14 @@ struct pt_context {
     bool coldPriority = true;         // pt_set_cold_start: issue priority on the cold start's order
     uint64_t stateEpoch = 0;          // bumped by every change of scene, textures, sky or RNG state
     uint64_t lastState = 0;           // stateEpoch at the last launch
+    // head groups: sample groups for the chain-bound head of the cost order
+    int headMode = 0;                 // pt_set_head_groups: 0 automatic, -1 off, K > 0 always K tiles
+    uint32_t headGroups = 2;          // groups per head tile
+    std::vector<uint32_t> sortedCost; // tile costs of the last order rebuild, descending (sort_order)
+    uint64_t orderSerial = 0;         // order rebuilds
+    uint64_t headPairsSerial = ~0ull; // orderSerial whose head tiles' draw-pair statistics were measured
+    uint32_t headPairsK = 0;
+    uint32_t lastHead = 0;            // head tiles of the last launch
     bool launched = false;
     float rootBox[6] = {};
     uint32_t nodeCount = 0, primCount = 0, stackDepth = 1;
@@ -2346,6 +2440,54 @@ static hipError_t launch_grouped(int v, const TraceParams& P, hipStream_t stream
     }
 }
 
+// Head-group launches (MODE 5, trace_head_kernel): the persistent grid of the variant's resident
+// workgroups, the scene staged in LDS as the variant does.
+template <int SL, int WPB, int WW, int MINW>
+static hipError_t launch_head_one(const TraceParams& P, hipStream_t stream)
+{
+    if (P.cnodes == nullptr) return hipErrorInvalidValue;
+    const size_t nodeF4 = 4 * (size_t)P.cnodeCount;
+    const size_t sceneBytes = ((SL >= 1 ? nodeF4 : 0) + (SL >= 2 ? 4 * (size_t)P.primCount : 0)) * sizeof(float4);
+    const size_t lds = sceneBytes + (size_t)WPB * P.stackDepth * 64 * 8 + (size_t)WPB * 64 * 12;
+    if (lds > 160 * 1024) {
+        if constexpr (SL > 0) return launch_head_one<0, WPB, WW, MINW>(P, stream);
+        else return hipErrorInvalidValue;
+    }
+    static std::atomic<uint64_t> attrSet{0};
+    static std::atomic<int> resident[64];
+    int dev = 0;
+    (void)hipGetDevice(&dev);
+    const uint64_t bit = 1ull << (dev & 63);
+    const void* fn = reinterpret_cast<const void*>(&trace_head_kernel<SL, WPB, WW, MINW>);
+    if (!(attrSet.load() & bit)) {
+        hipError_t e = hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+        if (e != hipSuccess) return e;
+        attrSet.fetch_or(bit);
+    }
+    int cap = resident[dev & 63].load();
+    if (cap == 0) {
+        int cus = 0, perCu = 0;
+        hipError_t e = hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
+        if (e == hipSuccess) e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&perCu, fn, WPB * 64, lds);
+        if (e != hipSuccess) return e;
+        cap = std::max(cus, 1) * std::max(perCu, 1);
+        resident[dev & 63].store(cap);
+    }
+    trace_head_kernel<SL, WPB, WW, MINW><<<(unsigned)cap, WPB * 64, lds, stream>>>(P);
+    return hipGetLastError();
+}
+
+static hipError_t launch_head(int v, const TraceParams& P, hipStream_t stream)
+{
+    switch (v) {
+    case 39: return launch_head_one<1, 4, 224, 5>(P, stream);
+    case 40: return launch_head_one<1, 4, kV40Walk, 5>(P, stream);
+    case 41: return launch_head_one<0, 4, 14212, 5>(P, stream);
+    case 46: return launch_head_one<0, 4, 14212, 4>(P, stream);
+    default: return hipErrorInvalidValue;
+    }
+}
+
 // Strip-unit launches (MODE 3) of the resumable persistent variants.
 static hipError_t launch_strip(int v, const TraceParams& P, hipStream_t stream)
 {
@@ -2404,6 +2546,10 @@ static bool variant_shipped(int v)
 // of the next call's first samples (the reference's render(cam, 8, ...) calls, main.cpp:272-279);
 // 1-2 spp progressive frames use strip units instead.
 constexpr uint64_t kAheadMinSamples = 3, kAheadMaxSamples = 64;
+// Head groups (render_impl): a plain launch is chain-bound when its most expensive tile costs more than
+// the work per wave slot (sum of the tile costs / resident waves); its tiles above kHeadAlpha of that
+// run as kHeadGroups-way sample groups in the same queue (at most a quarter of the slots' items).
+constexpr double kHeadAlpha = 0.95;
 constexpr uint32_t kPrepassSpp = 2;
 constexpr uint64_t kPrepassMinSpp = 16;
 
@@ -2902,16 +3048,21 @@ static int sort_order(pt_context* ctx, uint32_t tiles, uint64_t samples, uint32_
     size_t bytes = ctx->sortTempBytes;
     PT_HIP_CHECK(ctx, rocprim::radix_sort_pairs_desc(ctx->sortTemp, bytes, ctx->tileCost, ctx->sortKeys, ctx->tileIds,
                                                      ctx->order, tiles, 0, 32, ctx->stream));
+    // the sorted costs on the host too: the head-group decision (render_impl) reads the plateau
+    ctx->sortedCost.resize(tiles);
+    PT_HIP_CHECK(ctx, hipMemcpyAsync(ctx->sortedCost.data(), ctx->sortKeys, (size_t)tiles * sizeof(uint32_t),
+                                     hipMemcpyDeviceToHost, ctx->stream));
     PT_HIP_CHECK(ctx, hipStreamSynchronize(ctx->stream));
     ctx->orderValid = true;
     ctx->orderStale = false;
+    ++ctx->orderSerial;
     return PT_OK;
 }
 
 // Guess, grouped launch, fold, patch rounds and resume of speculative sample groups over the first
 // `groupTiles` tiles of P.order (all tiles when P.order is null), on `s`.
 static int run_groups(pt_context* ctx, int variant, const TraceParams& P0, uint32_t G, uint32_t groupTiles,
-                      uint32_t ssgCap, hipStream_t s)
+                      uint32_t ssgCap, hipStream_t s, uint32_t plainTiles = 0)
 {
     TraceParams P = P0;
     const uint32_t total = P.spp * P.chunks;
@@ -2936,7 +3087,15 @@ static int run_groups(pt_context* ctx, int variant, const TraceParams& P0, uint3
     PT_HIP_CHECK(ctx, hipGetLastError());
     P.ssgLook[0] = ctx->ssgLook[0];
     P.ssgLook[1] = ctx->ssgLook[1];
-    PT_HIP_CHECK(ctx, launch_grouped<1>(variant, P, s));
+    if (plainTiles) {
+        // head groups: the grouped items and the plain tiles after them in one persistent queue
+        TraceParams H = P;
+        H.headItems = (uint32_t)items;
+        H.numSlots = (uint32_t)items + plainTiles;
+        PT_HIP_CHECK(ctx, launch_head(variant, H, s));
+    } else {
+        PT_HIP_CHECK(ctx, launch_grouped<1>(variant, P, s));
+    }
     ssg_fold_kernel<<<pixBlocks, 256, 0, s>>>(P, 0, ctx->patchLog, ctx->patchEnd, ctx->patchCount, ssgCap, ctx->pairs,
                                               ctx->deadCount);
     PT_HIP_CHECK(ctx, hipGetLastError());
@@ -3203,9 +3362,41 @@ static int render_impl(pt_context* ctx, const pt_camera* cam, uint32_t spp, uint
                          (size_t)tiles * J * ssg_window_words(G, ssgN)))
             G = 0;
     }
+    // Head groups: a plain launch whose most expensive tile runs longer than the work
+    // per wave slot ends with that tile's sample chain (one rank's C4 share at N = 8: 474 ms against
+    // 412).  Its tiles above kHeadAlpha of the work per slot run as sample groups (items of a few
+    // hundred samples each) at the head of the same persistent queue, the rest plain behind them.
+    uint32_t headK = 0, headG = 0;
+    if (!G && !stats && sorted && ctx->orderValid && !ctx->orderStale && K == 1 && !ahead && !noRepair && groupable &&
+        ctx->headMode >= 0 && ctx->cnodes && (variant == 39 || variant == 40 || variant == 41 || variant == 46)) {
+        headG = std::max(2u, ctx->headGroups);
+        int cus = 0;
+        const uint64_t slots = hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, ctx->device) == hipSuccess
+                                   ? (uint64_t)cus * 4 * (variant == 46 ? 4 : 5) : 0;
+        if (ctx->headMode > 0) {
+            headK = std::min<uint32_t>((uint32_t)ctx->headMode, tiles);
+        } else if (slots && tiles >= 2 * slots && ctx->sortedCost.size() == tiles && total >= 64 * headG) {
+            // (launches of fewer tiles run every tile at once; sample groups, ssg_groups, serve those)
+            double sum = 0.0;
+            for (uint32_t c : ctx->sortedCost) sum += c;
+            const double perSlot = sum / (double)slots;
+            if ((double)ctx->sortedCost[0] > perSlot)
+                while (headK < tiles && (double)ctx->sortedCost[headK] > kHeadAlpha * perSlot) ++headK;
+            headK = std::min<uint64_t>(headK, slots / 4 / (2 * headG - 1));
+        }
+        if (headK) {
+            const uint32_t ssgN = total / headG;
+            ssgCap = std::min<uint32_t>({total, 2 * ssgN + 64, 10000u});
+            const size_t J = 2 * (size_t)headG - 1;
+            if (!ssg_reserve(ctx, tiles, (size_t)headK * J, (size_t)headK * J * ssgCap, (size_t)headK * ssgCap,
+                             (size_t)headK * J * ssg_window_words(headG, ssgN)))
+                headK = 0;
+        }
+    }
+    ctx->lastHead = headK;
     // a plain launch after grouped ones releases the group logs (a stream synchronisation and frees
     // of up to ~15 GB): before the timed region starts
-    if (!G) ssg_release(ctx);
+    if (!G && !headK) ssg_release(ctx);
     PT_HIP_CHECK(ctx, hipEventRecord(ctx->ev0, ctx->stream));
     // Cold start (first launch, or the scene, a texture or the camera changed): no tile costs yet.
     // Progressive 1-spp frames reuse the previous order for one launch.  A launch of several render()
@@ -3259,11 +3450,31 @@ static int render_impl(pt_context* ctx, const pt_camera* cam, uint32_t spp, uint
             biasedOrder = true;
         }
     }
-    if (G && P.tileCost) PT_HIP_CHECK(ctx, hipMemsetAsync(P.tileCost, 0, (size_t)tiles * sizeof(uint32_t), ctx->stream));
+    if ((G || headK) && P.tileCost) PT_HIP_CHECK(ctx, hipMemsetAsync(P.tileCost, 0, (size_t)tiles * sizeof(uint32_t), ctx->stream));
     if (G) {
         const int rc = run_groups(ctx, variant, P, G, tiles, ssgCap, ctx->stream);
         if (rc != PT_OK) return rc;
         ctx->lastGroups = G;
+    } else if (headK) {
+        if (ctx->headPairsSerial != ctx->orderSerial || headK > ctx->headPairsK) {
+            // the head tiles' draw pairs per sample for the groups' start guesses: an 8-spp pre-pass
+            // over them from the current state, nothing written back (the fold keeps them up to date)
+            TraceParams Q = P;
+            Q.spp = 8;
+            Q.chunks = 1;
+            Q.ignoreFirst = 1;
+            Q.discard = 1;
+            Q.numSlots = headK;
+            Q.tileCost = nullptr;
+            for (int i = 0; i < 3; ++i) Q.prio[i] = 0;
+            Q.pairsOut = ctx->pairs;
+            PT_HIP_CHECK(ctx, launch_grouped<2>(variant, Q, ctx->stream));
+            ctx->headPairsSerial = ctx->orderSerial;
+            ctx->headPairsK = headK;
+        }
+        const int rc = run_groups(ctx, variant, P, headG, headK, ssgCap, ctx->stream, tiles - headK);
+        if (rc != PT_OK) return rc;
+        ctx->lastGroups = headG;
     } else {
         PT_HIP_CHECK(ctx, stats ? launch_variant<true>(variant, P, ctx->stream)
                                 : ahead ? launch_ahead(variant, P, ctx->stream)
@@ -3326,6 +3537,16 @@ PT_API int pt_set_cold_start(pt_context* ctx, uint32_t prepass_spp, int priority
     ctx->coldPriority = priority != 0;
     return PT_OK;
 }
+
+PT_API int pt_set_head_groups(pt_context* ctx, int tiles, uint32_t groups)
+{
+    if (!ctx || tiles < -1 || groups == 1 || groups > 8) return PT_ERR_ARG;
+    ctx->headMode = tiles;
+    ctx->headGroups = groups ? groups : 2u;
+    return PT_OK;
+}
+
+PT_API int pt_last_head_tiles(const pt_context* ctx) { return ctx ? (int)ctx->lastHead : 0; }
 
 PT_API int pt_set_run_ahead(pt_context* ctx, int mode)
 {
