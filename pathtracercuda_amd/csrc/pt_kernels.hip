@@ -3323,7 +3323,8 @@ static int render_impl(pt_context* ctx, const pt_camera* cam, uint32_t spp, uint
     // the fold state packs (sample in call, call) into one word as sIdx | c << 16 (ssg_fold_kernel)
     const bool groupable = !stats && sorted && (uint64_t)spp * chunks < (1ull << 31) && spp <= 0xffffu && chunks <= 0xffffu;
     uint32_t G = groupable && K == 1 && !noRepair && !ahead ? ssg_groups(ctx, variant, tiles, total) : 0;
-    if (!G && ctx->variant == 0 && K == 1 && !noRepair && !ahead) variant = small_grid_variant(ctx, variant, tiles);
+    if (!G && ctx->variant == 0 && K == 1 && !noRepair && !ahead && ctx->headMode <= 0)   // (forced head groups
+        variant = small_grid_variant(ctx, variant, tiles);                                  //  keep the default walk)
     if (ahead) {
         if (!ctx->ahead) {
             const size_t n = std::max<size_t>((size_t)ctx->rows * ctx->width, 1);
