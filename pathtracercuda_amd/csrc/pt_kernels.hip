@@ -1785,24 +1785,31 @@ __global__ void __launch_bounds__(WPB * 64, MINW) trace_kernel(TraceParams P)
 // first `headTiles` tiles of the cost order (slots 0 .. headItems - 1, as a MODE 1 launch numbers
 // them) followed by the remaining tiles as plain tiles (MODE 0).  The two kinds of item run in
 // separate non-inlined functions, so each keeps the register allocation of its own instantiation
-// (a merged body spilled and slowed every tile); they read the launch parameters
-// through the kernel-argument pointer (scalar loads, as in the kernel).
+// (a merged body spilled and slowed every tile).  They read the launch parameters
+// through the kernel's argument-segment pointer, passed in and made scalar again (readfirstlane), so
+// every field is a scalar load from the constant address space as in the kernel itself.  (The
+// segment-pointer builtin is valid in the kernel only: a callee has no such input register.)
 typedef const __attribute__((address_space(4))) TraceParams* KernargParams;
 
-template <int SL, int WPB, int WW, int MINW>
-__device__ __noinline__ void head_group_item(uint32_t slot)
+PT_DEV const TraceParams& kernarg_params(KernargParams kp)
 {
-    const TraceParams& P = *(const TraceParams*)(KernargParams)__builtin_amdgcn_kernarg_segment_ptr();
-    Counters cnt = {};
-    run_item<false, SL, WPB, WW, MINW, true, 1>(P, slot, cnt);
+    const uint64_t a = (uint64_t)kp;
+    const uint32_t lo = __builtin_amdgcn_readfirstlane((uint32_t)a), hi = __builtin_amdgcn_readfirstlane((uint32_t)(a >> 32));
+    return *(const TraceParams*)(KernargParams)(((uint64_t)hi << 32) | lo);
 }
 
 template <int SL, int WPB, int WW, int MINW>
-__device__ __noinline__ void head_plain_item(uint32_t slot)
+__device__ __noinline__ void head_group_item(uint32_t slot, KernargParams kp)
 {
-    const TraceParams& P = *(const TraceParams*)(KernargParams)__builtin_amdgcn_kernarg_segment_ptr();
     Counters cnt = {};
-    run_item<false, SL, WPB, WW, MINW, true, 0>(P, slot, cnt);
+    run_item<false, SL, WPB, WW, MINW, true, 1>(kernarg_params(kp), slot, cnt);
+}
+
+template <int SL, int WPB, int WW, int MINW>
+__device__ __noinline__ void head_plain_item(uint32_t slot, KernargParams kp)
+{
+    Counters cnt = {};
+    run_item<false, SL, WPB, WW, MINW, true, 0>(kernarg_params(kp), slot, cnt);
 }
 
 template <int SL, int WPB, int WW, int MINW>
@@ -1810,11 +1817,12 @@ __global__ void __launch_bounds__(WPB * 64, MINW) trace_head_kernel(TraceParams 
 {
     const uint32_t wave = threadIdx.x >> 6;
     stage_scene_impl<SL, WPB, WW>(P);
+    const KernargParams kp = (KernargParams)__builtin_amdgcn_kernarg_segment_ptr();
     uint32_t slot = wave_fetch(P.tileCursor, 1u);
     (void)wave;
     while (slot < P.numSlots) {
-        if (slot < P.headItems) head_group_item<SL, WPB, WW, MINW>(slot);
-        else head_plain_item<SL, WPB, WW, MINW>(slot - P.headItems + P.ssgTiles);
+        if (slot < P.headItems) head_group_item<SL, WPB, WW, MINW>(slot, kp);
+        else head_plain_item<SL, WPB, WW, MINW>(slot - P.headItems + P.ssgTiles, kp);
         slot = wave_fetch(P.tileCursor, 1u);
     }
     if (wave_fetch(P.tileCursor + 1, 1u) == gridDim.x * (uint32_t)WPB - 1 && (threadIdx.x & 63u) == 0) {
