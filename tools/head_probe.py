@@ -46,7 +46,9 @@ for r in range(a.rounds):
         if ref is None:
             ref = acc.copy()
         ok = ok and np.array_equal(acc, ref)
-        print(json.dumps({"round": r, "setting": f"{k}:{g}", "ms": round(ms, 2), "head": pt.last_head_tiles}), flush=True)
+        gs = pt.group_stats() if pt.last_head_tiles else {}
+        print(json.dumps({"round": r, "setting": f"{k}:{g}", "ms": round(ms, 2), "head": pt.last_head_tiles,
+                          "group_stats": gs}), flush=True)
 out = {"share": f"{a.width}x{a.height}x{a.spp} N={a.n} rank {a.rank}", "bit_identical": bool(ok), "settings": {}}
 for key, d in res.items():
     out["settings"][key] = {"ms_median": float(np.median(d["ms"])), "ms": d["ms"], "head_tiles": d["head"]}
