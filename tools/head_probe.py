@@ -47,8 +47,18 @@ for r in range(a.rounds):
             ref = acc.copy()
         ok = ok and np.array_equal(acc, ref)
         gs = pt.group_stats() if pt.last_head_tiles else {}
+        extra = {}
+        costs = np.sort(pt.tile_costs().ravel().astype(np.float64) / 2.4e6)[::-1]    # ms (2.4 GHz)
+        extra["top_tile_ms"] = [round(float(x), 1) for x in costs[:5]]
+        if pt.last_head_tiles:
+            hk = pt.last_head_tiles
+            cnt = pt.group_log_counts()[:hk]                   # (head tiles, items, 64 lanes), order positions
+            per_item = cnt.max(axis=2)                         # slowest lane's samples per item
+            extra["item_max_samples_median"] = [int(np.median(per_item[:, j])) for j in range(per_item.shape[1])]
+            extra["item_max_samples_max"] = [int(per_item[:, j].max()) for j in range(per_item.shape[1])]
+            extra["items_at_cap"] = int((per_item >= a.spp).sum())
         print(json.dumps({"round": r, "setting": f"{k}:{g}", "ms": round(ms, 2), "head": pt.last_head_tiles,
-                          "group_stats": gs}), flush=True)
+                          "group_stats": gs, **extra}), flush=True)
 out = {"share": f"{a.width}x{a.height}x{a.spp} N={a.n} rank {a.rank}", "bit_identical": bool(ok), "settings": {}}
 for key, d in res.items():
     out["settings"][key] = {"ms_median": float(np.median(d["ms"])), "ms": d["ms"], "head_tiles": d["head"]}
