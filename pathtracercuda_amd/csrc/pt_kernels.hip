@@ -2238,7 +2238,7 @@ struct pt_context {
     uint64_t stateEpoch = 0;          // bumped by every change of scene, textures, sky or RNG state
     uint64_t lastState = 0;           // stateEpoch at the last launch
     // head groups: sample groups for the chain-bound head of the cost order
-    int headMode = 0;                 // pt_set_head_groups: 0 automatic, -1 off, K > 0 always K tiles
+    int headMode = -1;                // pt_set_head_groups: 0 automatic, -1 off (default until it measures faster), K > 0 always K tiles
     uint32_t headGroups = 2;          // groups per head tile
     std::vector<uint32_t> sortedCost; // tile costs of the last order rebuild, descending (sort_order)
     uint64_t orderSerial = 0;         // order rebuilds
