@@ -390,11 +390,11 @@ class Pathtracer:
 
     def group_log_counts(self) -> np.ndarray:
         """Samples each (tile, item) of the last grouped launch logged: (tiles, 2 * groups - 1, 64), tiles
-        in dispatch (cost) order; item 0 = group 0, items 2g - 1 and 2g = group g at its guess and one
+        in dispatch (cost) order (a head-group launch: its head tiles); item 0 = group 0, items 2g - 1 and 2g = group g at its guess and one
         draw pair later."""
         self._single("group_log_counts")
         g = 2 * self.last_sample_groups - 1
-        tiles = ((self.width + 7) // 8) * ((self.rows + 7) // 8)
+        tiles = self.last_head_tiles or ((self.width + 7) // 8) * ((self.rows + 7) // 8)
         out = np.zeros((tiles, g, 64), dtype=np.uint32)
         N.check_ctx(N.hip().pt_read_group_log_counts(self._ctx, out.ctypes.data_as(C.POINTER(C.c_uint32)), out.size),
                     self._ctx)

@@ -3610,7 +3610,8 @@ PT_API int pt_read_group_log_counts(pt_context* ctx, uint32_t* dst, size_t count
 {
     if (!ctx || !dst) return PT_ERR_ARG;
     if (!ctx->ssgCount || ctx->lastGroups == 0) return PT_ERR_STATE;
-    const size_t n = (size_t)((ctx->width + 7) / 8) * ((ctx->rows + 7) / 8) * (2 * ctx->lastGroups - 1) * 64;
+    const size_t tiles = ctx->lastHead ? ctx->lastHead : (size_t)((ctx->width + 7) / 8) * ((ctx->rows + 7) / 8);
+    const size_t n = tiles * (2 * ctx->lastGroups - 1) * 64;   // (a head-group launch: its head tiles)
     if (count < n) return PT_ERR_ARG;
     PT_HIP_CHECK(ctx, hipSetDevice(ctx->device));
     PT_HIP_CHECK(ctx, hipMemcpy(dst, ctx->ssgCount, n * sizeof(uint32_t), hipMemcpyDeviceToHost));
