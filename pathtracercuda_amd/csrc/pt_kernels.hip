@@ -118,6 +118,7 @@ struct TraceParams {
     uint32_t aheadMake;         // != 0: lanes whose pixel is done go on with the next call's samples
     uint32_t headItems;         // MODE 5 (trace_head_kernel): slots below this are sample-group items of the
                                 // first ssgTiles tiles, the rest plain tiles from order position ssgTiles on
+    uint32_t headInline;        // MODE 5 A/B: the plain tiles inlined in the kernel instead of a function
 };
 
 // Speculative sample groups: window of a group's start offset in which an earlier group's parse can
@@ -1820,8 +1821,10 @@ __global__ void __launch_bounds__(WPB * 64, MINW) trace_head_kernel(TraceParams 
     const KernargParams kp = (KernargParams)__builtin_amdgcn_kernarg_segment_ptr();
     uint32_t slot = wave_fetch(P.tileCursor, 1u);
     (void)wave;
+    Counters cnt = {};
     while (slot < P.numSlots) {
         if (slot < P.headItems) head_group_item<SL, WPB, WW, MINW>(slot, kp);
+        else if (P.headInline) run_item<false, SL, WPB, WW, MINW, true, 0>(P, slot - P.headItems + P.ssgTiles, cnt);
         else head_plain_item<SL, WPB, WW, MINW>(slot - P.headItems + P.ssgTiles, kp);
         slot = wave_fetch(P.tileCursor, 1u);
     }
@@ -3099,6 +3102,7 @@ static int run_groups(pt_context* ctx, int variant, const TraceParams& P0, uint3
         // head groups: the grouped items and the plain tiles after them in one persistent queue
         TraceParams H = P;
         H.headItems = (uint32_t)items;
+        H.headInline = ctx->headGroups >= 16 ? 1u : 0u;   // A/B knob: groups + 16
         H.numSlots = (uint32_t)items + plainTiles;
         PT_HIP_CHECK(ctx, launch_head(variant, H, s));
     } else {
@@ -3378,7 +3382,7 @@ static int render_impl(pt_context* ctx, const pt_camera* cam, uint32_t spp, uint
     uint32_t headK = 0, headG = 0;
     if (!G && !stats && sorted && ctx->orderValid && !ctx->orderStale && K == 1 && !ahead && !noRepair && groupable &&
         ctx->headMode >= 0 && ctx->cnodes && (variant == 39 || variant == 40 || variant == 41 || variant == 46)) {
-        headG = std::max(2u, ctx->headGroups);
+        headG = std::max(2u, ctx->headGroups & 15u);
         int cus = 0;
         const uint64_t slots = hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, ctx->device) == hipSuccess
                                    ? (uint64_t)cus * 4 * (variant == 46 ? 4 : 5) : 0;
@@ -3549,9 +3553,9 @@ PT_API int pt_set_cold_start(pt_context* ctx, uint32_t prepass_spp, int priority
 
 PT_API int pt_set_head_groups(pt_context* ctx, int tiles, uint32_t groups)
 {
-    if (!ctx || tiles < -1 || groups == 1 || groups > 8) return PT_ERR_ARG;
+    if (!ctx || tiles < -1 || groups == 1 || (groups > 8 && groups < 18) || groups > 24) return PT_ERR_ARG;
     ctx->headMode = tiles;
-    ctx->headGroups = groups ? groups : 2u;
+    ctx->headGroups = groups ? groups : 2u;            // (16 + G: A/B of the plain tiles inlined)
     return PT_OK;
 }
 
