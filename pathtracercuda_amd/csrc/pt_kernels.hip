@@ -2217,6 +2217,9 @@ __global__ void __launch_bounds__(256) unpermute_rows_kernel(float4* __restrict_
 struct pt_context {
     int device = 0;
     hipStream_t stream = nullptr;
+    hipStream_t stream2 = nullptr;    // head groups on two streams (run_groups)
+    hipEvent_t evHead = nullptr, evPlain = nullptr;
+    uint32_t* tileCursor2 = nullptr;
     hipEvent_t ev0 = nullptr, ev1 = nullptr;
     uint32_t width = 0, height = 0, rowOffset = 0, rowStride = 1, rows = 0, bandShift = 0;
     float4* accum = nullptr;
@@ -2728,6 +2731,10 @@ PT_API void pt_destroy(pt_context* ctx)
     if (ctx->ev0) (void)hipEventDestroy(ctx->ev0);
     if (ctx->ev1) (void)hipEventDestroy(ctx->ev1);
     if (ctx->stream) (void)hipStreamDestroy(ctx->stream);
+    if (ctx->stream2) (void)hipStreamDestroy(ctx->stream2);
+    if (ctx->evHead) (void)hipEventDestroy(ctx->evHead);
+    if (ctx->evPlain) (void)hipEventDestroy(ctx->evPlain);
+    (void)hipFree(ctx->tileCursor2);
     delete ctx;
 }
 
@@ -3098,7 +3105,31 @@ static int run_groups(pt_context* ctx, int variant, const TraceParams& P0, uint3
     PT_HIP_CHECK(ctx, hipGetLastError());
     P.ssgLook[0] = ctx->ssgLook[0];
     P.ssgLook[1] = ctx->ssgLook[1];
-    if (plainTiles) {
+    const bool twoStreams = plainTiles && ctx->headGroups >= 32;    // A/B knob: groups + 32
+    if (twoStreams) {
+        // head groups on two streams: the grouped items (non-persistent, their own cursor) on `s`,
+        // the plain kernel over the other tiles on a second stream, released once the guesses are in
+        // -- its persistent grid fills the slots the items leave free and takes theirs over when the
+        // items end; the fold and patch rounds follow the items on `s`
+        if (!ctx->stream2) PT_HIP_CHECK(ctx, hipStreamCreateWithFlags(&ctx->stream2, hipStreamNonBlocking));
+        if (!ctx->evHead) PT_HIP_CHECK(ctx, hipEventCreateWithFlags(&ctx->evHead, hipEventDisableTiming));
+        if (!ctx->evPlain) PT_HIP_CHECK(ctx, hipEventCreateWithFlags(&ctx->evPlain, hipEventDisableTiming));
+        if (!ctx->tileCursor2) {
+            PT_HIP_CHECK(ctx, hipMalloc(&ctx->tileCursor2, 2 * sizeof(uint32_t)));
+            PT_HIP_CHECK(ctx, hipMemset(ctx->tileCursor2, 0, 2 * sizeof(uint32_t)));
+        }
+        PT_HIP_CHECK(ctx, hipEventRecord(ctx->evHead, s));
+        PT_HIP_CHECK(ctx, hipStreamWaitEvent(ctx->stream2, ctx->evHead, 0));
+        TraceParams Gp = P;
+        Gp.tileCursor = ctx->tileCursor2;
+        PT_HIP_CHECK(ctx, launch_grouped<1>(variant, Gp, s));
+        TraceParams B = P0;
+        B.order = P0.order + groupTiles;
+        B.numSlots = plainTiles;
+        for (int i = 0; i < 3; ++i) B.prio[i] = P0.prio[i] > groupTiles ? P0.prio[i] - groupTiles : 0u;
+        PT_HIP_CHECK(ctx, launch_variant<false>(variant, B, ctx->stream2));
+        PT_HIP_CHECK(ctx, hipEventRecord(ctx->evPlain, ctx->stream2));
+    } else if (plainTiles) {
         // head groups: the grouped items and the plain tiles after them in one persistent queue
         TraceParams H = P;
         H.headItems = (uint32_t)items;
@@ -3141,6 +3172,7 @@ static int run_groups(pt_context* ctx, int variant, const TraceParams& P0, uint3
         R.tileCost = nullptr;
         PT_HIP_CHECK(ctx, launch_grouped<2>(variant, R, s));
     }
+    if (twoStreams) PT_HIP_CHECK(ctx, hipStreamWaitEvent(s, ctx->evPlain, 0));   // the plain tiles are done too
     return PT_OK;
 }
 
@@ -3382,7 +3414,7 @@ static int render_impl(pt_context* ctx, const pt_camera* cam, uint32_t spp, uint
     uint32_t headK = 0, headG = 0;
     if (!G && !stats && sorted && ctx->orderValid && !ctx->orderStale && K == 1 && !ahead && !noRepair && groupable &&
         ctx->headMode >= 0 && ctx->cnodes && (variant == 39 || variant == 40 || variant == 41 || variant == 46)) {
-        headG = std::max(2u, ctx->headGroups & 15u);
+        headG = std::max(2u, ctx->headGroups & 15u);      // (16 / 32 + G: A/B forms)
         int cus = 0;
         const uint64_t slots = hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, ctx->device) == hipSuccess
                                    ? (uint64_t)cus * 4 * (variant == 46 ? 4 : 5) : 0;
@@ -3553,7 +3585,8 @@ PT_API int pt_set_cold_start(pt_context* ctx, uint32_t prepass_spp, int priority
 
 PT_API int pt_set_head_groups(pt_context* ctx, int tiles, uint32_t groups)
 {
-    if (!ctx || tiles < -1 || groups == 1 || (groups > 8 && groups < 18) || groups > 24) return PT_ERR_ARG;
+    if (!ctx || tiles < -1 || groups == 1 || (groups > 8 && groups < 18) || (groups > 24 && groups < 34) || groups > 40)
+        return PT_ERR_ARG;
     ctx->headMode = tiles;
     ctx->headGroups = groups ? groups : 2u;            // (16 + G: A/B of the plain tiles inlined)
     return PT_OK;
