@@ -270,15 +270,6 @@ PT_API int pt_set_run_ahead(pt_context *ctx, int mode);
  * many spp.  priority: issue priority on that order (1, the default) or not (0).  Scheduling only:
  * results are identical for every setting. */
 PT_API int pt_set_cold_start(pt_context *ctx, uint32_t prepass_spp, int priority);
-/* Head groups: a plain launch whose most expensive tile costs more than the work per wave slot (its
- * sample chain would end the launch -- one rank's share of a 4K x 4096 image at N = 8) runs its tiles
- * above 0.95 x that work as `groups`-way speculative sample groups at the head of the same persistent
- * queue, the other tiles plain behind them.  tiles: 0 = automatic, -1 = off (the default: measured
- * slower so far), K > 0 = always the first K tiles of the cost order; groups: 0 = 2, else
- * 2..8.  Results are identical for every setting.  pt_last_head_tiles: the head tiles of the last
- * launch. */
-PT_API int pt_set_head_groups(pt_context *ctx, int tiles, uint32_t groups);
-PT_API int pt_last_head_tiles(const pt_context *ctx);
 PT_API int pt_set_sample_groups(pt_context *ctx, int mode);
 PT_API int pt_set_patch_rounds(pt_context *ctx, uint32_t rounds);
 PT_API int pt_set_group_lookback(pt_context *ctx, uint32_t far, uint32_t near);

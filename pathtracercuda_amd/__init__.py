@@ -329,17 +329,6 @@ class Pathtracer:
         for c in self._contexts():
             N.check_ctx(N.hip().pt_set_run_ahead(c, int(mode)), c)
 
-    def set_head_groups(self, tiles: int = 0, groups: int = 0) -> None:
-        """Head groups (pt_set_head_groups): 0 automatic, -1 off, K > 0 always the first K tiles of the
-        cost order as `groups`-way sample groups.  Results are identical for every setting."""
-        for c in self._contexts():
-            N.check_ctx(N.hip().pt_set_head_groups(c, int(tiles), int(groups)), c)
-
-    @property
-    def last_head_tiles(self) -> int:
-        """Head tiles of the last launch (a device group: the largest over its devices)."""
-        return max(int(N.hip().pt_last_head_tiles(c)) for c in self._contexts())
-
     def set_cold_start(self, prepass_spp: int = 0, priority: bool = True) -> None:
         """Cold-start scheduling (pt_set_cold_start): cost pre-pass spp (0 = default) and issue
         priority on the pre-pass's order.  Results are identical for every setting."""
@@ -390,11 +379,11 @@ class Pathtracer:
 
     def group_log_counts(self) -> np.ndarray:
         """Samples each (tile, item) of the last grouped launch logged: (tiles, 2 * groups - 1, 64), tiles
-        in dispatch (cost) order (a head-group launch: its head tiles); item 0 = group 0, items 2g - 1 and 2g = group g at its guess and one
+        in dispatch (cost) order; item 0 = group 0, items 2g - 1 and 2g = group g at its guess and one
         draw pair later."""
         self._single("group_log_counts")
         g = 2 * self.last_sample_groups - 1
-        tiles = self.last_head_tiles or ((self.width + 7) // 8) * ((self.rows + 7) // 8)
+        tiles = ((self.width + 7) // 8) * ((self.rows + 7) // 8)
         out = np.zeros((tiles, g, 64), dtype=np.uint32)
         N.check_ctx(N.hip().pt_read_group_log_counts(self._ctx, out.ctypes.data_as(C.POINTER(C.c_uint32)), out.size),
                     self._ctx)

@@ -76,8 +76,6 @@ _HIP_SYMBOLS = {
     "pt_set_rise_repair": (C.c_int, [C.c_void_p, C.c_int]),
     "pt_set_run_ahead": (C.c_int, [C.c_void_p, C.c_int]),
     "pt_set_cold_start": (C.c_int, [C.c_void_p, C.c_uint32, C.c_int]),
-    "pt_set_head_groups": (C.c_int, [C.c_void_p, C.c_int, C.c_uint32]),
-    "pt_last_head_tiles": (C.c_int, [C.c_void_p]),
     "pt_unpermute_bands": (C.c_int, [C.c_int, C.c_void_p, C.c_void_p, C.c_uint32, C.c_uint32, C.c_uint32, C.c_uint32,
                                      C.c_uint32]),
     "pt_set_kernel_variant": (C.c_int, [C.c_void_p, C.c_int]),

@@ -116,9 +116,6 @@ struct TraceParams {
     uint32_t* ahead;
     uint32_t aheadUse;          // != 0: the stash was made under this launch's camera and scene: consume it
     uint32_t aheadMake;         // != 0: lanes whose pixel is done go on with the next call's samples
-    uint32_t headItems;         // MODE 5 (trace_head_kernel): slots below this are sample-group items of the
-                                // first ssgTiles tiles, the rest plain tiles from order position ssgTiles on
-    uint32_t headInline;        // MODE 5 A/B: the plain tiles inlined in the kernel instead of a function
 };
 
 // Speculative sample groups: window of a group's start offset in which an earlier group's parse can
@@ -1735,10 +1732,8 @@ PT_DEV void run_item(const TraceParams& P, uint32_t slot, Counters& cnt)
     if (P.tileCost && lane == 0 && (tile >> 16) < P.tilesY) {
         const uint32_t cyc = (uint32_t)min(__builtin_amdgcn_s_memtime() - tWave, (uint64_t)0xffffffffu);
         const uint32_t lin = (tile >> 16) * P.tilesX + (tile & 0xffffu);
-        // SSG: zeroed before the launch (idle items add ~0); in a head-group launch the head tiles rank
-        // among plain tiles, so they record their longest item x groups, close to a plain run's cycles
-        if (SSG && P.headItems) atomicMax(&P.tileCost[lin], (uint32_t)min((uint64_t)cyc * P.ssgG, (uint64_t)0xffffffffu));
-        else if (SSG) atomicAdd(&P.tileCost[lin], cyc / P.ssgG);
+        // SSG: zeroed before the launch (idle items add ~0)
+        if (SSG) atomicAdd(&P.tileCost[lin], cyc / P.ssgG);
         else P.tileCost[lin] = cyc;
         // STRIP: the unit's cost sits at its first tile, the other tiles' entries are 0, so a sort of
         // the tile costs lists the units first (pt_render: the order of a strip launch)
@@ -1779,59 +1774,6 @@ __global__ void __launch_bounds__(WPB * 64, MINW) trace_kernel(TraceParams P)
         }
     }
     flush_counters<STATS>(P, cnt);
-}
-
-
-// Head groups (MODE 5): one persistent queue holding the sample-group items of the
-// first `headTiles` tiles of the cost order (slots 0 .. headItems - 1, as a MODE 1 launch numbers
-// them) followed by the remaining tiles as plain tiles (MODE 0).  The two kinds of item run in
-// separate non-inlined functions, so each keeps the register allocation of its own instantiation
-// (a merged body spilled and slowed every tile).  They read the launch parameters
-// through the kernel's argument-segment pointer, passed in and made scalar again (readfirstlane), so
-// every field is a scalar load from the constant address space as in the kernel itself.  (The
-// segment-pointer builtin is valid in the kernel only: a callee has no such input register.)
-typedef const __attribute__((address_space(4))) TraceParams* KernargParams;
-
-PT_DEV const TraceParams& kernarg_params(KernargParams kp)
-{
-    const uint64_t a = (uint64_t)kp;
-    const uint32_t lo = __builtin_amdgcn_readfirstlane((uint32_t)a), hi = __builtin_amdgcn_readfirstlane((uint32_t)(a >> 32));
-    return *(const TraceParams*)(KernargParams)(((uint64_t)hi << 32) | lo);
-}
-
-template <int SL, int WPB, int WW, int MINW>
-__device__ __noinline__ void head_group_item(uint32_t slot, KernargParams kp)
-{
-    Counters cnt = {};
-    run_item<false, SL, WPB, WW, MINW, true, 1>(kernarg_params(kp), slot, cnt);
-}
-
-template <int SL, int WPB, int WW, int MINW>
-__device__ __noinline__ void head_plain_item(uint32_t slot, KernargParams kp)
-{
-    Counters cnt = {};
-    run_item<false, SL, WPB, WW, MINW, true, 0>(kernarg_params(kp), slot, cnt);
-}
-
-template <int SL, int WPB, int WW, int MINW>
-__global__ void __launch_bounds__(WPB * 64, MINW) trace_head_kernel(TraceParams P)
-{
-    const uint32_t wave = threadIdx.x >> 6;
-    stage_scene_impl<SL, WPB, WW>(P);
-    const KernargParams kp = (KernargParams)__builtin_amdgcn_kernarg_segment_ptr();
-    uint32_t slot = wave_fetch(P.tileCursor, 1u);
-    (void)wave;
-    Counters cnt = {};
-    while (slot < P.numSlots) {
-        if (slot < P.headItems) head_group_item<SL, WPB, WW, MINW>(slot, kp);
-        else if (P.headInline) run_item<false, SL, WPB, WW, MINW, true, 0>(P, slot - P.headItems + P.ssgTiles, cnt);
-        else head_plain_item<SL, WPB, WW, MINW>(slot - P.headItems + P.ssgTiles, kp);
-        slot = wave_fetch(P.tileCursor, 1u);
-    }
-    if (wave_fetch(P.tileCursor + 1, 1u) == gridDim.x * (uint32_t)WPB - 1 && (threadIdx.x & 63u) == 0) {
-        P.tileCursor[0] = 0;
-        P.tileCursor[1] = 0;
-    }
 }
 
 // initRandState (initRandState.cu:4-17): curand_init(1984 + x + y * width, 0, 0)
@@ -2217,9 +2159,6 @@ __global__ void __launch_bounds__(256) unpermute_rows_kernel(float4* __restrict_
 struct pt_context {
     int device = 0;
     hipStream_t stream = nullptr;
-    hipStream_t stream2 = nullptr;    // head groups on two streams (run_groups)
-    hipEvent_t evHead = nullptr, evPlain = nullptr;
-    uint32_t* tileCursor2 = nullptr;
     hipEvent_t ev0 = nullptr, ev1 = nullptr;
     uint32_t width = 0, height = 0, rowOffset = 0, rowStride = 1, rows = 0, bandShift = 0;
     float4* accum = nullptr;
@@ -2243,14 +2182,6 @@ struct pt_context {
     bool coldPriority = true;         // pt_set_cold_start: issue priority on the cold start's order
     uint64_t stateEpoch = 0;          // bumped by every change of scene, textures, sky or RNG state
     uint64_t lastState = 0;           // stateEpoch at the last launch
-    // head groups: sample groups for the chain-bound head of the cost order
-    int headMode = -1;                // pt_set_head_groups: 0 automatic, -1 off (default until it measures faster), K > 0 always K tiles
-    uint32_t headGroups = 2;          // groups per head tile
-    std::vector<uint32_t> sortedCost; // tile costs of the last order rebuild, descending (sort_order)
-    uint64_t orderSerial = 0;         // order rebuilds
-    uint64_t headPairsSerial = ~0ull; // orderSerial whose head tiles' draw-pair statistics were measured
-    uint32_t headPairsK = 0;
-    uint32_t lastHead = 0;            // head tiles of the last launch
     bool launched = false;
     float rootBox[6] = {};
     uint32_t nodeCount = 0, primCount = 0, stackDepth = 1;
@@ -2454,54 +2385,6 @@ static hipError_t launch_grouped(int v, const TraceParams& P, hipStream_t stream
     }
 }
 
-// Head-group launches (MODE 5, trace_head_kernel): the persistent grid of the variant's resident
-// workgroups, the scene staged in LDS as the variant does.
-template <int SL, int WPB, int WW, int MINW>
-static hipError_t launch_head_one(const TraceParams& P, hipStream_t stream)
-{
-    if (P.cnodes == nullptr) return hipErrorInvalidValue;
-    const size_t nodeF4 = 4 * (size_t)P.cnodeCount;
-    const size_t sceneBytes = ((SL >= 1 ? nodeF4 : 0) + (SL >= 2 ? 4 * (size_t)P.primCount : 0)) * sizeof(float4);
-    const size_t lds = sceneBytes + (size_t)WPB * P.stackDepth * 64 * 8 + (size_t)WPB * 64 * 12;
-    if (lds > 160 * 1024) {
-        if constexpr (SL > 0) return launch_head_one<0, WPB, WW, MINW>(P, stream);
-        else return hipErrorInvalidValue;
-    }
-    static std::atomic<uint64_t> attrSet{0};
-    static std::atomic<int> resident[64];
-    int dev = 0;
-    (void)hipGetDevice(&dev);
-    const uint64_t bit = 1ull << (dev & 63);
-    const void* fn = reinterpret_cast<const void*>(&trace_head_kernel<SL, WPB, WW, MINW>);
-    if (!(attrSet.load() & bit)) {
-        hipError_t e = hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
-        if (e != hipSuccess) return e;
-        attrSet.fetch_or(bit);
-    }
-    int cap = resident[dev & 63].load();
-    if (cap == 0) {
-        int cus = 0, perCu = 0;
-        hipError_t e = hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
-        if (e == hipSuccess) e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&perCu, fn, WPB * 64, lds);
-        if (e != hipSuccess) return e;
-        cap = std::max(cus, 1) * std::max(perCu, 1);
-        resident[dev & 63].store(cap);
-    }
-    trace_head_kernel<SL, WPB, WW, MINW><<<(unsigned)cap, WPB * 64, lds, stream>>>(P);
-    return hipGetLastError();
-}
-
-static hipError_t launch_head(int v, const TraceParams& P, hipStream_t stream)
-{
-    switch (v) {
-    case 39: return launch_head_one<1, 4, 224, 5>(P, stream);
-    case 40: return launch_head_one<1, 4, kV40Walk, 5>(P, stream);
-    case 41: return launch_head_one<0, 4, 14212, 5>(P, stream);
-    case 46: return launch_head_one<0, 4, 14212, 4>(P, stream);
-    default: return hipErrorInvalidValue;
-    }
-}
-
 // Strip-unit launches (MODE 3) of the resumable persistent variants.
 static hipError_t launch_strip(int v, const TraceParams& P, hipStream_t stream)
 {
@@ -2554,16 +2437,12 @@ static bool variant_shipped(int v)
            v == 91;   // 91: variant 48 without the rising-t_max rebuild (A/B of its cost only; not the reference's bits)
 }
 
-// Cost pre-pass of a cold-start launch (render_impl): samples per pixel, and the smallest launch
-// (spp x chunks) that gets one.
 // Run-ahead (MODE 4): launches of kAheadMinSamples..kAheadMaxSamples samples per pixel make a stash
 // of the next call's first samples (the reference's render(cam, 8, ...) calls, main.cpp:272-279);
 // 1-2 spp progressive frames use strip units instead.
 constexpr uint64_t kAheadMinSamples = 3, kAheadMaxSamples = 64;
-// Head groups (render_impl): a plain launch is chain-bound when its most expensive tile costs more than
-// the work per wave slot (sum of the tile costs / resident waves); its tiles above kHeadAlpha of that
-// run as kHeadGroups-way sample groups in the same queue (at most a quarter of the slots' items).
-constexpr double kHeadAlpha = 0.95;
+// Cost pre-pass of a cold-start launch (render_impl): samples per pixel, and the smallest launch
+// (spp x chunks) that gets one.
 constexpr uint32_t kPrepassSpp = 2;
 constexpr uint64_t kPrepassMinSpp = 16;
 
@@ -2731,10 +2610,6 @@ PT_API void pt_destroy(pt_context* ctx)
     if (ctx->ev0) (void)hipEventDestroy(ctx->ev0);
     if (ctx->ev1) (void)hipEventDestroy(ctx->ev1);
     if (ctx->stream) (void)hipStreamDestroy(ctx->stream);
-    if (ctx->stream2) (void)hipStreamDestroy(ctx->stream2);
-    if (ctx->evHead) (void)hipEventDestroy(ctx->evHead);
-    if (ctx->evPlain) (void)hipEventDestroy(ctx->evPlain);
-    (void)hipFree(ctx->tileCursor2);
     delete ctx;
 }
 
@@ -3066,21 +2941,16 @@ static int sort_order(pt_context* ctx, uint32_t tiles, uint64_t samples, uint32_
     size_t bytes = ctx->sortTempBytes;
     PT_HIP_CHECK(ctx, rocprim::radix_sort_pairs_desc(ctx->sortTemp, bytes, ctx->tileCost, ctx->sortKeys, ctx->tileIds,
                                                      ctx->order, tiles, 0, 32, ctx->stream));
-    // the sorted costs on the host too: the head-group decision (render_impl) reads the plateau
-    ctx->sortedCost.resize(tiles);
-    PT_HIP_CHECK(ctx, hipMemcpyAsync(ctx->sortedCost.data(), ctx->sortKeys, (size_t)tiles * sizeof(uint32_t),
-                                     hipMemcpyDeviceToHost, ctx->stream));
     PT_HIP_CHECK(ctx, hipStreamSynchronize(ctx->stream));
     ctx->orderValid = true;
     ctx->orderStale = false;
-    ++ctx->orderSerial;
     return PT_OK;
 }
 
 // Guess, grouped launch, fold, patch rounds and resume of speculative sample groups over the first
 // `groupTiles` tiles of P.order (all tiles when P.order is null), on `s`.
 static int run_groups(pt_context* ctx, int variant, const TraceParams& P0, uint32_t G, uint32_t groupTiles,
-                      uint32_t ssgCap, hipStream_t s, uint32_t plainTiles = 0)
+                      uint32_t ssgCap, hipStream_t s)
 {
     TraceParams P = P0;
     const uint32_t total = P.spp * P.chunks;
@@ -3105,40 +2975,7 @@ static int run_groups(pt_context* ctx, int variant, const TraceParams& P0, uint3
     PT_HIP_CHECK(ctx, hipGetLastError());
     P.ssgLook[0] = ctx->ssgLook[0];
     P.ssgLook[1] = ctx->ssgLook[1];
-    const bool twoStreams = plainTiles && ctx->headGroups >= 32;    // A/B knob: groups + 32
-    if (twoStreams) {
-        // head groups on two streams: the grouped items (non-persistent, their own cursor) on `s`,
-        // the plain kernel over the other tiles on a second stream, released once the guesses are in
-        // -- its persistent grid fills the slots the items leave free and takes theirs over when the
-        // items end; the fold and patch rounds follow the items on `s`
-        if (!ctx->stream2) PT_HIP_CHECK(ctx, hipStreamCreateWithFlags(&ctx->stream2, hipStreamNonBlocking));
-        if (!ctx->evHead) PT_HIP_CHECK(ctx, hipEventCreateWithFlags(&ctx->evHead, hipEventDisableTiming));
-        if (!ctx->evPlain) PT_HIP_CHECK(ctx, hipEventCreateWithFlags(&ctx->evPlain, hipEventDisableTiming));
-        if (!ctx->tileCursor2) {
-            PT_HIP_CHECK(ctx, hipMalloc(&ctx->tileCursor2, 2 * sizeof(uint32_t)));
-            PT_HIP_CHECK(ctx, hipMemset(ctx->tileCursor2, 0, 2 * sizeof(uint32_t)));
-        }
-        PT_HIP_CHECK(ctx, hipEventRecord(ctx->evHead, s));
-        PT_HIP_CHECK(ctx, hipStreamWaitEvent(ctx->stream2, ctx->evHead, 0));
-        TraceParams Gp = P;
-        Gp.tileCursor = ctx->tileCursor2;
-        PT_HIP_CHECK(ctx, launch_grouped<1>(variant, Gp, s));
-        TraceParams B = P0;
-        B.order = P0.order + groupTiles;
-        B.numSlots = plainTiles;
-        for (int i = 0; i < 3; ++i) B.prio[i] = P0.prio[i] > groupTiles ? P0.prio[i] - groupTiles : 0u;
-        PT_HIP_CHECK(ctx, launch_variant<false>(variant, B, ctx->stream2));
-        PT_HIP_CHECK(ctx, hipEventRecord(ctx->evPlain, ctx->stream2));
-    } else if (plainTiles) {
-        // head groups: the grouped items and the plain tiles after them in one persistent queue
-        TraceParams H = P;
-        H.headItems = (uint32_t)items;
-        H.headInline = ctx->headGroups >= 16 ? 1u : 0u;   // A/B knob: groups + 16
-        H.numSlots = (uint32_t)items + plainTiles;
-        PT_HIP_CHECK(ctx, launch_head(variant, H, s));
-    } else {
-        PT_HIP_CHECK(ctx, launch_grouped<1>(variant, P, s));
-    }
+    PT_HIP_CHECK(ctx, launch_grouped<1>(variant, P, s));
     ssg_fold_kernel<<<pixBlocks, 256, 0, s>>>(P, 0, ctx->patchLog, ctx->patchEnd, ctx->patchCount, ssgCap, ctx->pairs,
                                               ctx->deadCount);
     PT_HIP_CHECK(ctx, hipGetLastError());
@@ -3172,7 +3009,6 @@ static int run_groups(pt_context* ctx, int variant, const TraceParams& P0, uint3
         R.tileCost = nullptr;
         PT_HIP_CHECK(ctx, launch_grouped<2>(variant, R, s));
     }
-    if (twoStreams) PT_HIP_CHECK(ctx, hipStreamWaitEvent(s, ctx->evPlain, 0));   // the plain tiles are done too
     return PT_OK;
 }
 
@@ -3367,8 +3203,7 @@ static int render_impl(pt_context* ctx, const pt_camera* cam, uint32_t spp, uint
     // the fold state packs (sample in call, call) into one word as sIdx | c << 16 (ssg_fold_kernel)
     const bool groupable = !stats && sorted && (uint64_t)spp * chunks < (1ull << 31) && spp <= 0xffffu && chunks <= 0xffffu;
     uint32_t G = groupable && K == 1 && !noRepair && !ahead ? ssg_groups(ctx, variant, tiles, total) : 0;
-    if (!G && ctx->variant == 0 && K == 1 && !noRepair && !ahead && ctx->headMode <= 0)   // (forced head groups
-        variant = small_grid_variant(ctx, variant, tiles);                                  //  keep the default walk)
+    if (!G && ctx->variant == 0 && K == 1 && !noRepair && !ahead) variant = small_grid_variant(ctx, variant, tiles);
     if (ahead) {
         if (!ctx->ahead) {
             const size_t n = std::max<size_t>((size_t)ctx->rows * ctx->width, 1);
@@ -3407,41 +3242,9 @@ static int render_impl(pt_context* ctx, const pt_camera* cam, uint32_t spp, uint
                          (size_t)tiles * J * ssg_window_words(G, ssgN)))
             G = 0;
     }
-    // Head groups: a plain launch whose most expensive tile runs longer than the work
-    // per wave slot ends with that tile's sample chain (one rank's C4 share at N = 8: 474 ms against
-    // 412).  Its tiles above kHeadAlpha of the work per slot run as sample groups (items of a few
-    // hundred samples each) at the head of the same persistent queue, the rest plain behind them.
-    uint32_t headK = 0, headG = 0;
-    if (!G && !stats && sorted && ctx->orderValid && !ctx->orderStale && K == 1 && !ahead && !noRepair && groupable &&
-        ctx->headMode >= 0 && ctx->cnodes && (variant == 39 || variant == 40 || variant == 41 || variant == 46)) {
-        headG = std::max(2u, ctx->headGroups & 15u);      // (16 / 32 + G: A/B forms)
-        int cus = 0;
-        const uint64_t slots = hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, ctx->device) == hipSuccess
-                                   ? (uint64_t)cus * 4 * (variant == 46 ? 4 : 5) : 0;
-        if (ctx->headMode > 0) {
-            headK = std::min<uint32_t>((uint32_t)ctx->headMode, tiles);
-        } else if (slots && tiles >= 2 * slots && ctx->sortedCost.size() == tiles && total >= 64 * headG) {
-            // (launches of fewer tiles run every tile at once; sample groups, ssg_groups, serve those)
-            double sum = 0.0;
-            for (uint32_t c : ctx->sortedCost) sum += c;
-            const double perSlot = sum / (double)slots;
-            if ((double)ctx->sortedCost[0] > perSlot)
-                while (headK < tiles && (double)ctx->sortedCost[headK] > kHeadAlpha * perSlot) ++headK;
-            headK = std::min<uint64_t>(headK, slots / 4 / (2 * headG - 1));
-        }
-        if (headK) {
-            const uint32_t ssgN = total / headG;
-            ssgCap = std::min<uint32_t>({total, 2 * ssgN + 64, 10000u});
-            const size_t J = 2 * (size_t)headG - 1;
-            if (!ssg_reserve(ctx, tiles, (size_t)headK * J, (size_t)headK * J * ssgCap, (size_t)headK * ssgCap,
-                             (size_t)headK * J * ssg_window_words(headG, ssgN)))
-                headK = 0;
-        }
-    }
-    ctx->lastHead = headK;
     // a plain launch after grouped ones releases the group logs (a stream synchronisation and frees
     // of up to ~15 GB): before the timed region starts
-    if (!G && !headK) ssg_release(ctx);
+    if (!G) ssg_release(ctx);
     PT_HIP_CHECK(ctx, hipEventRecord(ctx->ev0, ctx->stream));
     // Cold start (first launch, or the scene, a texture or the camera changed): no tile costs yet.
     // Progressive 1-spp frames reuse the previous order for one launch.  A launch of several render()
@@ -3495,31 +3298,11 @@ static int render_impl(pt_context* ctx, const pt_camera* cam, uint32_t spp, uint
             biasedOrder = true;
         }
     }
-    if ((G || headK) && P.tileCost) PT_HIP_CHECK(ctx, hipMemsetAsync(P.tileCost, 0, (size_t)tiles * sizeof(uint32_t), ctx->stream));
+    if (G && P.tileCost) PT_HIP_CHECK(ctx, hipMemsetAsync(P.tileCost, 0, (size_t)tiles * sizeof(uint32_t), ctx->stream));
     if (G) {
         const int rc = run_groups(ctx, variant, P, G, tiles, ssgCap, ctx->stream);
         if (rc != PT_OK) return rc;
         ctx->lastGroups = G;
-    } else if (headK) {
-        if (ctx->headPairsSerial != ctx->orderSerial || headK > ctx->headPairsK) {
-            // the head tiles' draw pairs per sample for the groups' start guesses: an 8-spp pre-pass
-            // over them from the current state, nothing written back (the fold keeps them up to date)
-            TraceParams Q = P;
-            Q.spp = 8;
-            Q.chunks = 1;
-            Q.ignoreFirst = 1;
-            Q.discard = 1;
-            Q.numSlots = headK;
-            Q.tileCost = nullptr;
-            for (int i = 0; i < 3; ++i) Q.prio[i] = 0;
-            Q.pairsOut = ctx->pairs;
-            PT_HIP_CHECK(ctx, launch_grouped<2>(variant, Q, ctx->stream));
-            ctx->headPairsSerial = ctx->orderSerial;
-            ctx->headPairsK = headK;
-        }
-        const int rc = run_groups(ctx, variant, P, headG, headK, ssgCap, ctx->stream, tiles - headK);
-        if (rc != PT_OK) return rc;
-        ctx->lastGroups = headG;
     } else {
         PT_HIP_CHECK(ctx, stats ? launch_variant<true>(variant, P, ctx->stream)
                                 : ahead ? launch_ahead(variant, P, ctx->stream)
@@ -3583,17 +3366,6 @@ PT_API int pt_set_cold_start(pt_context* ctx, uint32_t prepass_spp, int priority
     return PT_OK;
 }
 
-PT_API int pt_set_head_groups(pt_context* ctx, int tiles, uint32_t groups)
-{
-    if (!ctx || tiles < -1 || groups == 1 || (groups > 8 && groups < 18) || (groups > 24 && groups < 34) || groups > 40)
-        return PT_ERR_ARG;
-    ctx->headMode = tiles;
-    ctx->headGroups = groups ? groups : 2u;            // (16 + G: A/B of the plain tiles inlined)
-    return PT_OK;
-}
-
-PT_API int pt_last_head_tiles(const pt_context* ctx) { return ctx ? (int)ctx->lastHead : 0; }
-
 PT_API int pt_set_run_ahead(pt_context* ctx, int mode)
 {
     if (!ctx || mode < 0 || mode > 3) return PT_ERR_ARG;
@@ -3647,8 +3419,8 @@ PT_API int pt_read_group_log_counts(pt_context* ctx, uint32_t* dst, size_t count
 {
     if (!ctx || !dst) return PT_ERR_ARG;
     if (!ctx->ssgCount || ctx->lastGroups == 0) return PT_ERR_STATE;
-    const size_t tiles = ctx->lastHead ? ctx->lastHead : (size_t)((ctx->width + 7) / 8) * ((ctx->rows + 7) / 8);
-    const size_t n = tiles * (2 * ctx->lastGroups - 1) * 64;   // (a head-group launch: its head tiles)
+    const size_t tiles = (size_t)((ctx->width + 7) / 8) * ((ctx->rows + 7) / 8);
+    const size_t n = tiles * (2 * ctx->lastGroups - 1) * 64;
     if (count < n) return PT_ERR_ARG;
     PT_HIP_CHECK(ctx, hipSetDevice(ctx->device));
     PT_HIP_CHECK(ctx, hipMemcpy(dst, ctx->ssgCount, n * sizeof(uint32_t), hipMemcpyDeviceToHost));

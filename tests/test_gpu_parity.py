@@ -882,44 +882,3 @@ def test_run_ahead_modes_same_bits_full_frame(gpu_available, scenes):
     pt.set_rng_state(st)
     pt.render(cam, 8, True, chunks=24)
     assert np.array_equal(pt.accum().view(np.uint32), want[0]) and np.array_equal(pt.rng_state(), want[1])
-
-
-@pytest.mark.parametrize("K,G", [(12, 2), (40, 3), (96, 2)])
-def test_head_groups_bitexact_vs_oracle(gpu_available, scenes, K, G):
-    # head groups (MODE 5, trace_head_kernel): the first K tiles of the cost order run as G-way sample
-    # groups at the head of the persistent queue, the other tiles plain behind them, in one launch;
-    # two launches with history, against the oracle (accumulation and RNG state)
-    W, H = 200, 152
-    pt, cam, ref, osc = pair(scenes / "generated_scene.scene.json", W, H)
-    pt.set_run_ahead(1)
-    pt.render(cam, 8, True)                    # cost order (a head launch needs a warm order)
-    ref.render(osc.camera, 8, True)
-    pt.set_head_groups(K, G)
-    for ignore in (False, False):
-        pt.render(cam, 8, ignore, chunks=16)
-        assert pt.last_head_tiles == min(K, ((W + 7) // 8) * ((H + 7) // 8))
-        ref.render(osc.camera, 8, ignore, chunks=16)
-        assert_bitexact(pt.accum(), ref.accum, f"head groups K={K} G={G}")
-        assert np.array_equal(pt.rng_state(), ref.rng_array())
-
-
-def test_head_groups_large_grid_match_plain(gpu_available, scenes):
-    # the persistent head kernel on a grid of more tiles than resident waves, forced and automatic,
-    # bit-identical to the plain launch over several launches (a band share of the 4K image)
-    W, H = 3840, 2160
-    pt = pa.Pathtracer(W, H, row_offset=3, row_stride=8, band_rows=8)
-    cam = pt.load_scene(scenes / "generated_scene.scene.json")
-    pt.render(cam, 8, True, chunks=4)
-    st = pt.rng_state()
-    want = None
-    for mode, groups in ((-1, 0), (300, 2), (200, 3), (0, 2)):
-        pt.set_head_groups(mode, groups)
-        pt.set_rng_state(st)
-        pt.render(cam, 8, True, chunks=16)
-        pt.render(cam, 8, False, chunks=16)
-        if mode > 0:
-            assert pt.last_head_tiles == mode
-        got = (pt.accum().view(np.uint32).copy(), pt.rng_state())
-        if want is None:
-            want = got
-        assert np.array_equal(got[0], want[0]) and np.array_equal(got[1], want[1]), (mode, groups)
