@@ -206,8 +206,8 @@ PT_API int pt_read_tile_costs(pt_context *ctx, uint32_t *dst, uint32_t count);
 PT_API int pt_read_tile_idle(pt_context *ctx, uint32_t *dst, uint32_t count);
 
 /* Tuning knob for A/B measurements: 0 = automatic (default); otherwise one of the shipped
- * trace-kernel variants 1, 4, 6, 20, 39, 40, 41, 46, 47, 48 (traversal loop shape, deferred shading,
- * BVH staged in LDS or read through the caches, occupancy target; see pt_kernels.hip).  All variants
+ * trace-kernel variants 1, 4, 6, 20, 39, 40, 41, 46, 47, 48, 60, 61 (traversal loop shape, deferred
+ * shading, BVH staged in LDS or read through the caches, occupancy target; see pt_kernels.hip).  All variants
  * produce bit-identical results.  Other numbers return PT_ERR_ARG. */
 PT_API int pt_set_kernel_variant(pt_context *ctx, int variant);
 
@@ -274,6 +274,8 @@ PT_API int pt_set_sample_groups(pt_context *ctx, int mode);
 PT_API int pt_set_patch_rounds(pt_context *ctx, uint32_t rounds);
 PT_API int pt_set_group_lookback(pt_context *ctx, uint32_t far, uint32_t near);
 PT_API int pt_last_sample_groups(const pt_context *ctx);
+/* The trace-kernel variant the last launch ran (its main pass; diagnostics and tests). */
+PT_API int pt_last_variant(const pt_context *ctx);
 PT_API int pt_read_group_stats(const pt_context *ctx, uint32_t *dst);
 PT_API int pt_read_group_log_counts(pt_context *ctx, uint32_t *dst, size_t count);
 /* Diagnostics: one word plane of the per-pixel fold state (rows x width; word 16 = dead-end flag,

@@ -351,6 +351,11 @@ class Pathtracer:
         """Groups of the last launch (a device group: the largest over its devices)."""
         return max(int(N.hip().pt_last_sample_groups(c)) for c in self._contexts())
 
+    @property
+    def last_variant(self) -> int:
+        """Trace-kernel variant of the last launch's main pass (a device group: device 0's)."""
+        return int(N.hip().pt_last_variant(self._contexts()[0]))
+
     def set_patch_rounds(self, rounds: int) -> None:
         for c in self._contexts():
             N.check_ctx(N.hip().pt_set_patch_rounds(c, int(rounds)), c)

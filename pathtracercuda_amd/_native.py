@@ -84,6 +84,7 @@ _HIP_SYMBOLS = {
     "pt_set_schedule": (C.c_int, [C.c_void_p, C.c_int]),
     "pt_set_sample_groups": (C.c_int, [C.c_void_p, C.c_int]),
     "pt_last_sample_groups": (C.c_int, [C.c_void_p]),
+    "pt_last_variant": (C.c_int, [C.c_void_p]),
     "pt_read_group_stats": (C.c_int, [C.c_void_p, P(C.c_uint32)]),
     "pt_set_patch_rounds": (C.c_int, [C.c_void_p, C.c_uint32]),
     "pt_set_group_lookback": (C.c_int, [C.c_void_p, C.c_uint32, C.c_uint32]),

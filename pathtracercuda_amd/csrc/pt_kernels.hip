@@ -2233,6 +2233,7 @@ struct pt_context {
     size_t ssgItems = 0, ssgSamples = 0, patchSamples = 0;   // allocated capacities (records)
     size_t ssgBitsWords = 0;
     uint32_t lastGroups = 0;      // groups of the last launch (0 = plain launch)
+    int lastVariant = 0;          // trace-kernel variant of the last launch's main pass
     uint32_t groupStats[10] = {}; // G, patch rounds, dead-end pixels after fold rounds 0..7
     pt_camera lastCam = {};
     uint64_t epoch = 0;           // launches that wrote the accumulation (a group's gather cache key)
@@ -2365,6 +2366,12 @@ static hipError_t launch_variant(int v, const TraceParams& P, hipStream_t stream
     case 46: return launch_one<STATS, 0, 4, 14212, 4, true, MODE>(P, stream);
     case 47: return launch_one<STATS, 1, 4, 224, 4, true, MODE>(P, stream);
     case 48: return launch_one<STATS, 2, 4, 13216, 4, true, MODE>(P, stream);
+    case 60:
+        if constexpr (STATS) return launch_one<STATS, 1, 4, kV40Walk, 5, true, MODE>(P, stream);
+        else return launch_one<false, 1, 8, kV40Walk, 6, true, MODE>(P, stream);
+    case 61:
+        if constexpr (STATS) return launch_one<STATS, 0, 4, 14212, 5, true, MODE>(P, stream);
+        else return launch_one<false, 0, 4, 14212, 6, true, MODE>(P, stream);
     case 90: return launch_one<false, 1, 4, 100000 + kV40Walk, 5, true, 0>(P, stream);   // test only: 40, no repair
     case 91: return launch_one<false, 2, 4, 113216, 4, true, 0>(P, stream);              // A/B only: 48, no repair
     default: return hipErrorInvalidValue;
@@ -2381,6 +2388,8 @@ static hipError_t launch_grouped(int v, const TraceParams& P, hipStream_t stream
     case 40: return launch_one<false, 1, 4, kV40Walk, 5, true, MODE>(P, stream);
     case 41: return launch_one<false, 0, 4, 14212, 5, true, MODE>(P, stream);
     case 46: return launch_one<false, 0, 4, 14212, 4, true, MODE>(P, stream);
+    case 60: return launch_one<false, 1, 8, kV40Walk, 6, true, MODE>(P, stream);
+    case 61: return launch_one<false, 0, 4, 14212, 6, true, MODE>(P, stream);
     default: return hipErrorInvalidValue;
     }
 }
@@ -2392,11 +2401,16 @@ static hipError_t launch_strip(int v, const TraceParams& P, hipStream_t stream)
     case 40: return launch_one<false, 1, 4, kV40Walk, 5, true, 3>(P, stream);
     case 41: return launch_one<false, 0, 4, 14212, 5, true, 3>(P, stream);
     case 46: return launch_one<false, 0, 4, 14212, 4, true, 3>(P, stream);
+    case 60: return launch_one<false, 1, 8, kV40Walk, 6, true, 3>(P, stream);
+    case 61: return launch_one<false, 0, 4, 14212, 6, true, 3>(P, stream);
     default: return hipErrorInvalidValue;
     }
 }
 
-static bool strip_capable(int v) { return v == 40 || v == 41 || v == 46; }
+static bool strip_capable(int v) { return v == 40 || v == 41 || v == 46 || v == 60 || v == 61; }
+
+// Waves per SIMD a persistent variant is compiled for (its wave slots: CUs x 4 SIMDs x this).
+static uint32_t variant_waves(int v) { return v == 60 || v == 61 ? 6u : (v == 46 || v == 47 || v == 48 || v == 91) ? 4u : 5u; }
 
 // Run-ahead launches (MODE 4) of the resumable persistent variants.
 static hipError_t launch_ahead(int v, const TraceParams& P, hipStream_t stream)
@@ -2405,6 +2419,8 @@ static hipError_t launch_ahead(int v, const TraceParams& P, hipStream_t stream)
     case 40: return launch_one<false, 1, 4, kV40Walk, 5, true, 4>(P, stream);
     case 41: return launch_one<false, 0, 4, 14212, 5, true, 4>(P, stream);
     case 46: return launch_one<false, 0, 4, 14212, 4, true, 4>(P, stream);
+    case 60: return launch_one<false, 1, 8, kV40Walk, 6, true, 4>(P, stream);
+    case 61: return launch_one<false, 0, 4, 14212, 6, true, 4>(P, stream);
     default: return hipErrorInvalidValue;
     }
 }
@@ -2427,14 +2443,14 @@ static uint32_t strip_tiles(const pt_context* ctx, int variant, uint32_t tiles, 
     if (samples > kStripMaxSamples) return 1;
     int cus = 0;
     if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, ctx->device) != hipSuccess) return 1;
-    const uint64_t slots = (uint64_t)cus * 4 * 5;
+    const uint64_t slots = (uint64_t)cus * 4 * 5;       // (the threshold was measured at five waves)
     return (uint64_t)tiles >= 6 * slots ? 4u : 1u;
 }
 
 static bool variant_shipped(int v)
 {
     return v == 0 || v == 1 || v == 4 || v == 6 || v == 20 || v == 40 || v == 41 || v == 46 || v == 47 || v == 48 || v == 39 ||
-           v == 91;   // 91: variant 48 without the rising-t_max rebuild (A/B of its cost only; not the reference's bits)
+           v == 60 || v == 61 || v == 91;   // 91: variant 48 without the rising-t_max rebuild (A/B of its cost only; not the reference's bits)
 }
 
 // Run-ahead (MODE 4): launches of kAheadMinSamples..kAheadMaxSamples samples per pixel make a stash
@@ -2467,12 +2483,20 @@ static int pick_variant(const pt_context* ctx)
     // A cache-read scene whose four LDS stacks per workgroup leave room for fewer than five
     // workgroups per CU (BVH depth > 16) runs at 4 waves/SIMD anyway: variant 46 is variant 41
     // compiled for that occupancy (128 VGPRs, no spill), +1% on the 100k-object scene (depth 19).
+    // Six waves per SIMD (variants 60 / 61: the same walks compiled for 80 VGPRs) when the LDS holds
+    // them: with the records in LDS as three 8-wave workgroups per CU (the records staged once per
+    // eight waves), with cache-read records as six 4-wave workgroups.  Measured on C3
+    // (profiles/r05_six_waves.json): 60 224.2 ms against 40 231.2; 61 237.5 against 41 245.7.
     const size_t cbBytes = 4 * (size_t)ctx->cnodeCount * sizeof(float4);
-    const size_t groupBytes = 4 * (size_t)ctx->stackDepth * 64 * 8 + 4 * 64 * 12;   // stacks + accumulation slices
+    const size_t waveBytes = (size_t)ctx->stackDepth * 64 * 8 + 64 * 12;   // a wave's stack + accumulation slice
+    const size_t ldsCap = 160 * 1024;
     // (a BVH whose leaves are not in DFS primitive order cannot be descended by repair_pending: the
     // node-at-a-time walks, which push every far child as the reference does)
-    if (ctx->cnodes && ctx->dfsOrder) return cbBytes <= 48 * 1024 ? 40 : (5 * groupBytes > 160 * 1024 ? 46 : 41);
-    return nodeBytes <= 48 * 1024 ? 6 : 4;
+    if (!ctx->cnodes || !ctx->dfsOrder) return nodeBytes <= 48 * 1024 ? 6 : 4;
+    if (cbBytes <= 48 * 1024 && 3 * (cbBytes + 8 * waveBytes) <= ldsCap) return 60;
+    if (cbBytes <= 48 * 1024 && 5 * (cbBytes + 4 * waveBytes) <= ldsCap) return 40;
+    if (6 * 4 * waveBytes <= ldsCap) return 61;
+    return cbBytes <= 48 * 1024 ? 40 : (5 * 4 * waveBytes > ldsCap ? 46 : 41);
 }
 
 extern "C" {
@@ -2820,11 +2844,11 @@ PT_API int pt_set_skybox(pt_context* ctx, uint32_t handle)
 // (1.5 tiles per slot or more: the cost-sorted list schedule balances well enough).
 static uint32_t ssg_groups(const pt_context* ctx, int variant, uint32_t tiles, uint32_t total)
 {
-    if (ctx->ssgMode == 1 || (variant != 39 && variant != 40 && variant != 41 && variant != 46)) return 0;
+    if (ctx->ssgMode == 1 || !(variant == 39 || strip_capable(variant))) return 0;
     if (ctx->ssgMode >= 2) return std::min<uint32_t>((uint32_t)ctx->ssgMode, std::max(total, 1u));
     int cus = 0;
     if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, ctx->device) != hipSuccess) return 0;
-    const uint64_t resident = (uint64_t)cus * 4 * (variant == 46 ? 4 : 5);
+    const uint64_t resident = (uint64_t)cus * 4 * variant_waves(variant);
     uint64_t g = (6 * resident + tiles - 1) / tiles;
     g = std::min<uint64_t>({g, 8, total / 64});
     // measured (tools/ssg_probe.py): with 2 or 3 groups the logging, the fold and the
@@ -2843,8 +2867,8 @@ static int small_grid_variant(const pt_context* ctx, int variant, uint32_t tiles
     int cus = 0;
     if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, ctx->device) != hipSuccess) return variant;
     if ((uint64_t)tiles > (uint64_t)cus * 4 * 4) return variant;
-    if (variant == 41) return 46;
-    if (variant != 40) return variant;
+    if (variant == 41 || variant == 61) return 46;
+    if (variant != 40 && variant != 60) return variant;
     const size_t group = 4 * (size_t)ctx->cnodeCount * sizeof(float4) + 4 * (size_t)ctx->primCount * sizeof(float4) +
                          4 * (size_t)ctx->stackDepth * 64 * 8 + 4 * 64 * 12;
     return 4 * group <= 160 * 1024 ? 48 : 47;
@@ -3204,6 +3228,17 @@ static int render_impl(pt_context* ctx, const pt_camera* cam, uint32_t spp, uint
     const bool groupable = !stats && sorted && (uint64_t)spp * chunks < (1ull << 31) && spp <= 0xffffu && chunks <= 0xffffu;
     uint32_t G = groupable && K == 1 && !noRepair && !ahead ? ssg_groups(ctx, variant, tiles, total) : 0;
     if (!G && ctx->variant == 0 && K == 1 && !noRepair && !ahead) variant = small_grid_variant(ctx, variant, tiles);
+    // The sixth wave slot (variants 60 / 61) raises throughput but gives each wave a smaller share of
+    // the SIMD's issue: a plain launch of few tiles per slot, whose end is its heaviest tiles' sample
+    // chains, runs longer with it (the C4 N = 8 share, 2.6 tiles per six-wave slot: 532 against 498 ms;
+    // C3, 5.3 tiles per slot: 224.2 against 231.2; profiles/r05_six_waves.json).  Plain launches of
+    // fewer than 4 dispatch units per six-wave slot (also 1-spp strip-unit frames) run the five-wave build.
+    if (!G && ctx->variant == 0 && (variant == 60 || variant == 61)) {
+        int cus = 0;
+        if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, ctx->device) != hipSuccess ||
+            (uint64_t)units < 4ull * cus * 4 * 6)
+            variant = variant == 60 ? 40 : 41;
+    }
     if (ahead) {
         if (!ctx->ahead) {
             const size_t n = std::max<size_t>((size_t)ctx->rows * ctx->width, 1);
@@ -3214,6 +3249,7 @@ static int render_impl(pt_context* ctx, const pt_camera* cam, uint32_t spp, uint
         P.aheadMake = aheadMake ? 1u : 0u;
     }
     if (noRepair) {
+        if (variant == 60) variant = 40;              // (the no-repair build exists at five waves only)
         if (variant != 40 || stats)
             return fail(ctx, PT_ERR_STATE, "pt_set_rise_repair(0): only plain launches of variant 40 have a no-repair build");
         variant = 90;
@@ -3222,13 +3258,14 @@ static int render_impl(pt_context* ctx, const pt_camera* cam, uint32_t spp, uint
     // short items whose latency sets the launch: deferred shading, which trades a lane's latency for
     // fuller hit-shading rounds, measured bimodal there (median 57.7-62.6 ms against 57.8-58.2 ms
     // without; at N = 4, two tiles per slot, 96.8 against 103.9), so they run the undeferred walk.
-    if (G && ctx->variant == 0 && variant == 40) {
+    if (G && ctx->variant == 0 && (variant == 40 || variant == 60)) {
         int cus = 0;
         if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, ctx->device) == hipSuccess &&
-            (uint64_t)tiles <= (uint64_t)cus * 4 * 5)
+            (uint64_t)tiles <= (uint64_t)cus * 4 * variant_waves(variant))
             variant = 39;
     }
     ctx->lastGroups = 0;
+    ctx->lastVariant = variant;
     memset(ctx->groupStats, 0, sizeof(ctx->groupStats));
     ++ctx->epoch;
     uint32_t ssgCap = 0;
@@ -3413,6 +3450,8 @@ PT_API int pt_last_sample_groups(const pt_context* ctx)
 {
     return ctx ? (int)ctx->lastGroups : 0;
 }
+
+PT_API int pt_last_variant(const pt_context* ctx) { return ctx ? ctx->lastVariant : 0; }
 
 
 PT_API int pt_read_group_log_counts(pt_context* ctx, uint32_t* dst, size_t count)

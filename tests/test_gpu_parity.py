@@ -31,7 +31,7 @@ def assert_bitexact(gpu, ref, what):
                          f"ref={ref[y, x]}; max L2 {e.max():.3g}, pixels > 1e-4: {(e > 1e-4).mean():.2%}")
 
 
-SHIPPED_VARIANTS = (1, 4, 6, 20, 39, 40, 41, 46, 47, 48)
+SHIPPED_VARIANTS = (1, 4, 6, 20, 39, 40, 41, 46, 47, 48, 60, 61)
 
 
 def pair(scene_path, W, H, row_offset=0, row_stride=1, band_rows=1):
@@ -93,7 +93,7 @@ def test_persistent_variants_large_grid(gpu_available, scenes):
     pt.set_kernel_variant(1)
     pt.render(cam, 3, True, chunks=3)
     want = pt.accum().view(np.uint32).copy()       # bits: the reference's NaN pixels stay NaN
-    for variant in (39, 40, 41, 46, 47, 48):
+    for variant in (39, 40, 41, 46, 47, 48, 60, 61):
         pt.set_kernel_variant(variant)
         pt.set_rng_state(st)
         pt.render(cam, 3, True, chunks=3)
@@ -643,7 +643,7 @@ def test_walk_variants_full_frame_match(gpu_available, scenes):
     pt.set_strip_units(1)
     st = pt.rng_state()
     want = None
-    for variant in (40, 39, 41, 46, 20):
+    for variant in (40, 39, 41, 46, 20, 60, 61):
         pt.set_kernel_variant(variant)
         pt.set_rng_state(st)
         for i in range(16):
@@ -694,13 +694,13 @@ def test_rise_repair_runs_and_is_exact_vs_oracle(gpu_available, scenes):
     ref.render(osc.camera, spp, True, chunks=chunks, collect_stats=True)
     rises = int(ref.stats[7])
     assert rises > 0
-    for variant in (0, 40, 20):
+    for variant in (0, 40, 20, 60):
         pt.set_kernel_variant(variant)
         pt.set_rng_state(st)
         pt.render_raw(cam, spp, chunks, True)
         assert_bitexact(pt.accum(), ref.accum, f"rise scene, variant {variant}")
         assert np.array_equal(pt.rng_state(), ref.rng_array()), f"rise scene, variant {variant}: RNG"
-    for variant in (40, 20):
+    for variant in (40, 20, 60):
         pt.set_kernel_variant(variant)
         pt.set_rng_state(st)
         stats = pt.render_instrumented(cam, spp, chunks, True)
@@ -739,13 +739,13 @@ def test_rise_pair_needs_the_repair(gpu_available, scenes):
     N.check_ctx(N.hip().pt_set_scene(pt._ctx, _bvh_array(nodes), len(nodes),
                                      (pa.PtHittable * len(order)).from_buffer_copy(raw), len(order)), pt._ctx)
     st = pt.rng_state()
-    for variant in (0, 40, 41, 39, 20, 1):
+    for variant in (0, 40, 41, 39, 20, 1, 60, 61):
         pt.set_kernel_variant(variant)
         pt.set_rng_state(st)
         pt.render_raw(cam, spp, chunks, True)
         assert_bitexact(pt.accum(), ref.accum, f"rise pair, variant {variant}")
         assert np.array_equal(pt.rng_state(), ref.rng_array()), f"rise pair, variant {variant}: RNG"
-    for variant in (40, 20):
+    for variant in (40, 20, 60):
         pt.set_kernel_variant(variant)
         pt.set_rng_state(st)
         assert pt.render_instrumented(cam, spp, chunks, True)["repairs"] == rises, variant
@@ -797,7 +797,7 @@ def test_orphan_node_bvh_renders_exactly(gpu_available, scenes):
     ref.render(osc.camera, 4, True, chunks=2)
     _set_caller_bvh(pt, osc, bad)
     st = pt.rng_state()
-    for variant in (0, 40, 41, 39, 20):
+    for variant in (0, 40, 41, 39, 20, 60, 61):
         pt.set_kernel_variant(variant)
         pt.set_rng_state(st)
         pt.render_raw(cam, 4, 2, True)
@@ -822,7 +822,7 @@ def test_forced_strip_variant_without_child_box_layout(gpu_available, scenes):
     N.check_ctx(N.hip().pt_set_scene(pt._ctx, nodes, 1, prims, osc.prim_count), pt._ctx)
     ref.render(osc.camera, 1, True, chunks=2)
     st = pt.rng_state()
-    for variant in (40, 41, 46):
+    for variant in (40, 41, 46, 60, 61):
         pt.set_kernel_variant(variant)
         pt.set_strip_units(4)
         pt.set_rng_state(st)
@@ -882,3 +882,24 @@ def test_run_ahead_modes_same_bits_full_frame(gpu_available, scenes):
     pt.set_rng_state(st)
     pt.render(cam, 8, True, chunks=24)
     assert np.array_equal(pt.accum().view(np.uint32), want[0]) and np.array_equal(pt.rng_state(), want[1])
+
+
+def test_six_wave_policy(gpu_available, scenes):
+    # the default runs the six-wave build (variant 60) on a
+    # launch of many tiles per slot and the five-wave build on a chain-bound share of few tiles per
+    # slot; the bits are the same either way
+    pt = pa.Pathtracer(1920, 1080)
+    cam = pt.load_scene(scenes / "generated_scene.scene.json")
+    st = pt.rng_state()
+    pt.render_raw(cam, 8, 16, True)
+    assert pt.last_variant == 60
+    want = pt.accum().view(np.uint32).copy()
+    pt.set_kernel_variant(40)
+    pt.set_rng_state(st)
+    pt.render_raw(cam, 8, 16, True)
+    assert pt.last_variant == 40 and np.array_equal(pt.accum().view(np.uint32), want)
+    share = pa.Pathtracer(1920, 1080, row_offset=0, row_stride=2, band_rows=8)
+    cam = share.load_scene(scenes / "generated_scene.scene.json")
+    share.set_sample_groups(1)
+    share.render_raw(cam, 8, 16, True)
+    assert share.last_variant == 40

@@ -34,7 +34,7 @@ def same(a, b, what):
     ("generated_scene", 96, 54, 8, 16, 8),
     ("test_shapes", 80, 50, 8, 8, 3),
 ])
-@pytest.mark.parametrize("variant", [39, 40])          # grouped walk without / with deferred shading
+@pytest.mark.parametrize("variant", [39, 40, 60, 61])  # grouped walk without / with deferred shading, 6 waves
 def test_groups_bitexact_vs_oracle(gpu_available, scenes, name, W, H, spp, chunks, groups, variant):
     p = scenes / f"{name}.scene.json"
     pt = pa.Pathtracer(W, H)

@@ -27,6 +27,8 @@ def main():
     ap.add_argument("--n", type=int, default=1, help="render one rank's share of an N-way 8-row band partition")
     ap.add_argument("--rank", type=int, default=0)
     ap.add_argument("--groups", type=int, default=1, help="sample groups: 1 = off (plain launches), 0 = automatic")
+    ap.add_argument("--block", type=int, default=1,
+                    help="launches per variant per round; with > 1 the first of each block (after a switch) is dropped")
     ap.add_argument("--check", type=int, default=1, help="assert every variant bit-identical (0 for A/B-only variants)")
     a = ap.parse_args()
     if a.scene == "stress_100k":                   # C5's generated scene (bench.scene_path)
@@ -40,6 +42,7 @@ def main():
     chunks = a.spp // 8
     ref = None
     times = {v: [] for v in vs}
+    ran = {}
     for v, m in vs:                                # correctness first: every variant bit-identical
         pt.set_kernel_variant(v)
         pt.set_schedule(m)
@@ -58,14 +61,17 @@ def main():
             if len(a.schedules.split(",")) > 1:
                 pt.set_schedule(m)
                 pt.render_raw(cam, 8, 1, True)     # records the tile costs for mode 0
-            ms = pt.render_raw(cam, 8, chunks, True)
-            times[(v, m)].append(ms)
+            for b in range(a.block):
+                ms = pt.render_raw(cam, 8, chunks, True)
+                if b or a.block == 1:            # blocks: the first launch after a switch is not kept
+                    times[(v, m)].append(ms)
+            ran[(v, m)] = pt.last_variant
     samples = a.width * pt.rows * a.spp
     out = {}
     for v, m in vs:
         t = np.array(times[(v, m)])
         key = f"{v}" + ("" if len(a.schedules.split(",")) == 1 else f"/s{m}")
-        out[key] = {"median_ms": float(np.median(t)), "min_ms": float(t.min()),
+        out[key] = {"median_ms": float(np.median(t)), "min_ms": float(t.min()), "ran": ran[(v, m)], "ms": [round(x, 2) for x in t],
                     "Msamples_s": round(samples / (np.median(t) / 1e3) / 1e6, 1)}
     print(json.dumps({"scene": pathlib.Path(a.scene).name, "image": f"{a.width}x{a.height}", "spp": a.spp,
                       "n": a.n, "rank": a.rank, "variants": out}))
