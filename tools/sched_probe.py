@@ -49,12 +49,13 @@ def main():
     ap.add_argument("--width", type=int, default=1920)
     ap.add_argument("--height", type=int, default=1080)
     ap.add_argument("--spp", type=int, default=1024)
-    ap.add_argument("--n", type=int, default=1, help="rank 0's share of an N-way 8-row band partition")
+    ap.add_argument("--n", type=int, default=1, help="a rank's share of an N-way 8-row band partition")
+    ap.add_argument("--rank", type=int, default=0)
     ap.add_argument("--scheds", default="p0,p256")
     ap.add_argument("--rounds", type=int, default=3)
     ap.add_argument("--groups", type=int, default=1, help="sample groups: 1 = off, 0 = automatic")
     a = ap.parse_args()
-    pt = (pa.Pathtracer(a.width, a.height, row_offset=0, row_stride=a.n, band_rows=8) if a.n > 1
+    pt = (pa.Pathtracer(a.width, a.height, row_offset=a.rank, row_stride=a.n, band_rows=8) if a.n > 1
           else pa.Pathtracer(a.width, a.height))
     pt.set_sample_groups(a.groups)
     cam = pt.load_scene(a.scene)
