@@ -15,7 +15,8 @@
 //     sample as soon as a path ends, so a wave stays busy until its lanes have finished all
 //     samples of all chunks of the launch, instead of idling at every path end;
 //   * all `chunks` render() calls of the headless loop run in one launch; the per-chunk summation
-//     (color = sum of spp paths, then color + accum) is reproduced exactly in registers;
+//     (color = sum of spp paths, then color + accum) is reproduced exactly (the colour sum in LDS,
+//     the accumulation value in registers);
 //   * RNG state (24 B/pixel) and accum (16 B/pixel) are read once and written once per launch, SoA;
 //   * the BVH node test hoists the per-ray reciprocals (bit-identical to recomputing them) and the
 //     hit record is reconstructed once for the closest hit instead of for every candidate hit.
@@ -1003,9 +1004,9 @@ PT_DEV f3 specular_ggx(f3 F0, float NdotV, float NdotL, float NdotH, float VdotH
 struct PathState {
     f3 o, d;          // current ray
     f3 L, T;          // radiance and throughput of the current path (trace.cu:104-105)
-    f3 color;         // sum of the finished paths of the current render() call (trace.cu:186)
-    uint32_t acc;     // float index of this lane's running accumulation value in the dynamic LDS
-                      // (x, y, z at lds_f()[acc], [acc + 64], [acc + 128])
+    f3 accum;         // running accumulation value (trace.cu:196), folded once per render() call
+    uint32_t col;     // float index in the dynamic LDS of the sum of the finished paths of the current
+                      // render() call (trace.cu:186): x, y, z at lds_f()[col], [col + 64], [col + 128]
     uint32_t s, c, bounce;
     bool alive;
 };
@@ -1162,6 +1163,24 @@ PT_DEV PixelCtx pixel_of(const TraceParams& P, uint32_t tile, uint32_t lane)
     return pc;
 }
 
+// The current render() call's colour sum lives in the wave's LDS slice (touched once per sample),
+// the running accumulation value in registers (touched once per call): with six waves per SIMD
+// (80 VGPRs) the register allocator spills the value used least often, and a per-call spill costs
+// an eighth of a per-sample one at the reference's 8 spp per call.
+PT_DEV f3 get_color(const PathState& ps)
+{
+    const float* c = lds_f() + ps.col;
+    return mk(c[0], c[64], c[128]);
+}
+
+PT_DEV void set_color(const PathState& ps, const f3& v)
+{
+    float* c = lds_f() + ps.col;
+    c[0] = v.x;
+    c[64] = v.y;
+    c[128] = v.z;
+}
+
 template <bool AUX, bool AHEAD = false>
 PT_DEV void load_pixel(const TraceParams& P, const PixelCtx& pc, Xorwow& rng, PathState& ps, uint32_t accL)
 {
@@ -1172,28 +1191,27 @@ PT_DEV void load_pixel(const TraceParams& P, const PixelCtx& pc, Xorwow& rng, Pa
     rng.v2 = P.rng[3 * pc.npix + pc.li];
     rng.v3 = P.rng[4 * pc.npix + pc.li];
     rng.v4 = P.rng[5 * pc.npix + pc.li];
-    ps.acc = accL;
+    ps.col = accL;
+    ps.accum = splat(0.0f);
     if (!P.ignoreFirst || (AUX && P.fold)) {     // the first call of an ignoreHistory launch overwrites it
         const float4 a = P.accum[pc.li];
-        float* l = lds_f() + accL;
-        l[0] = a.x;
-        l[64] = a.y;
-        l[128] = a.z;
+        ps.accum = mk(a.x, a.y, a.z);
     }
-    ps.color = splat(0.0f);
+    f3 color = splat(0.0f);
     ps.L = splat(0.0f);
     ps.T = splat(1.0f);
     ps.s = ps.c = ps.bounce = 0;
     ps.alive = P.chunks > 0 && P.spp > 0;
     if (AUX && P.fold) {                         // mid-launch state left by ssg_fold_kernel
         const uint32_t* F = P.fold;
-        ps.color = mk(__uint_as_float(F[(F_COL + 0) * pc.npix + pc.li]), __uint_as_float(F[(F_COL + 1) * pc.npix + pc.li]),
-                      __uint_as_float(F[(F_COL + 2) * pc.npix + pc.li]));
+        color = mk(__uint_as_float(F[(F_COL + 0) * pc.npix + pc.li]), __uint_as_float(F[(F_COL + 1) * pc.npix + pc.li]),
+                   __uint_as_float(F[(F_COL + 2) * pc.npix + pc.li]));
         const uint32_t sc = F[F_SC * pc.npix + pc.li];
         ps.s = sc & 0xffffu;
         ps.c = sc >> 16;
         ps.alive = ps.c < P.chunks;
     }
+    set_color(ps, color);
 }
 
 // Run-ahead (MODE 4): the previous launch's stash of this call's first k samples (same camera, scene,
@@ -1205,7 +1223,7 @@ PT_DEV void ahead_load(const TraceParams& P, const PixelCtx& pc, Xorwow& rng, Pa
     const size_t n = pc.npix, li = pc.li;
     const uint32_t k = A[3 * n + li];
     if (k == 0u || k > P.spp) return;
-    ps.color = mk(__uint_as_float(A[li]), __uint_as_float(A[n + li]), __uint_as_float(A[2 * n + li]));
+    set_color(ps, mk(__uint_as_float(A[li]), __uint_as_float(A[n + li]), __uint_as_float(A[2 * n + li])));
     ps.s = k;
     rng.d = A[4 * n + li];
     rng.v0 = A[5 * n + li];
@@ -1228,8 +1246,7 @@ PT_DEV void store_pixel(const TraceParams& P, const PixelCtx& pc, const Xorwow& 
     P.rng[3 * pc.npix + li] = rng.v2;
     P.rng[4 * pc.npix + li] = rng.v3;
     P.rng[5 * pc.npix + li] = rng.v4;
-    const float* a = lds_f() + ps.acc;
-    P.accum[li] = make_float4(a[0], a[64], a[128], 1.0f);   // trace.cu:198, once per launch
+    P.accum[li] = make_float4(ps.accum.x, ps.accum.y, ps.accum.z, 1.0f);   // trace.cu:198, once per launch
 }
 
 // Run-ahead (MODE 4): after every sample of the NEXT call a lane stashes the call's colour sum so far
@@ -1266,19 +1283,15 @@ PT_DEV void ahead_store(const TraceParams& P, const PixelCtx& pc, const f3& colo
 template <bool AHEAD>
 PT_DEV void end_call(const TraceParams& P, const PixelCtx& pc, PathState& ps, const Xorwow& rng)
 {
+    const f3 color = get_color(ps);
     if (AHEAD && ps.c == P.chunks) {
-        ahead_store(P, pc, ps.color, ps.s, rng);
+        ahead_store(P, pc, color, ps.s, rng);
         ps.alive = false;
         return;
     }
     const bool ignore = (ps.c == 0) && P.ignoreFirst;
-    f3 acc = ps.color;
-    float* a = lds_f() + ps.acc;
-    if (!ignore) acc = add(ps.color, mk(a[0], a[64], a[128]));
-    a[0] = acc.x;
-    a[64] = acc.y;
-    a[128] = acc.z;
-    ps.color = splat(0.0f);
+    ps.accum = ignore ? color : add(color, ps.accum);
+    set_color(ps, splat(0.0f));
     ps.s = 0;
     if (++ps.c == P.chunks) {
         ps.alive = false;
@@ -1294,10 +1307,11 @@ template <bool STATS, bool AHEAD = false>
 PT_DEV void finish_path(const TraceParams& P, PathState& ps, Xorwow& rng, float fx, float fy, Counters& cnt,
                         const PixelCtx& pc)
 {
-    ps.color = add(ps.color, ps.L);
+    const f3 color = add(get_color(ps), ps.L);
+    set_color(ps, color);
     if (STATS) cnt.samples++;
     if (++ps.s == P.spp) end_call<AHEAD>(P, pc, ps, rng);
-    else if (AHEAD && ps.c == P.chunks) ahead_store(P, pc, ps.color, ps.s, rng);   // a next-call sample
+    else if (AHEAD && ps.c == P.chunks) ahead_store(P, pc, color, ps.s, rng);   // a next-call sample
     if (ps.alive) {
         camera_ray(P, fx, fy, rng, ps.o, ps.d);
         ps.L = splat(0.0f);
