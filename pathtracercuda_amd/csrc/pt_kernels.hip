@@ -1004,9 +1004,10 @@ PT_DEV f3 specular_ggx(f3 F0, float NdotV, float NdotL, float NdotH, float VdotH
 struct PathState {
     f3 o, d;          // current ray
     f3 L, T;          // radiance and throughput of the current path (trace.cu:104-105)
-    f3 accum;         // running accumulation value (trace.cu:196), folded once per render() call
-    uint32_t col;     // float index in the dynamic LDS of the sum of the finished paths of the current
-                      // render() call (trace.cu:186): x, y, z at lds_f()[col], [col + 64], [col + 128]
+    f3 sum;           // CL builds: the running accumulation value (trace.cu:196); else the sum of the
+                      // finished paths of the current render() call (trace.cu:186) -- see get_color
+    uint32_t slot;    // float index of this lane's slice of the dynamic LDS holding the other of the
+                      // two: x, y, z at lds_f()[slot], [slot + 64], [slot + 128]
     uint32_t s, c, bounce;
     bool alive;
 };
@@ -1163,25 +1164,43 @@ PT_DEV PixelCtx pixel_of(const TraceParams& P, uint32_t tile, uint32_t lane)
     return pc;
 }
 
-// The current render() call's colour sum lives in the wave's LDS slice (touched once per sample),
-// the running accumulation value in registers (touched once per call): with six waves per SIMD
-// (80 VGPRs) the register allocator spills the value used least often, and a per-call spill costs
-// an eighth of a per-sample one at the reference's 8 spp per call.
-PT_DEV f3 get_color(const PathState& ps)
+// Where the current render() call's colour sum (touched once per sample) and the running
+// accumulation value (touched once per call) live.  CL (the six-wave builds, 80 VGPRs): the colour
+// sum in the wave's LDS slice, the accumulation value in registers -- the register allocator spills
+// the value used least often, and a per-call spill costs an eighth of a per-sample one at the
+// reference's 8 spp per call (C3 224.2 -> 221.7 ms).  Otherwise the reverse: the five- and four-wave
+// builds have the registers, and an LDS round trip per sample cost the deep-BVH build (4 waves/SIMD)
+// 2.6 % (profiles/r05_six_waves.json).
+PT_DEV f3 slice_get(const PathState& ps)
 {
-    const float* c = lds_f() + ps.col;
+    const float* c = lds_f() + ps.slot;
     return mk(c[0], c[64], c[128]);
 }
 
-PT_DEV void set_color(const PathState& ps, const f3& v)
+PT_DEV void slice_set(const PathState& ps, const f3& v)
 {
-    float* c = lds_f() + ps.col;
+    float* c = lds_f() + ps.slot;
     c[0] = v.x;
     c[64] = v.y;
     c[128] = v.z;
 }
 
-template <bool AUX, bool AHEAD = false>
+template <bool CL> PT_DEV f3 get_color(const PathState& ps) { return CL ? slice_get(ps) : ps.sum; }
+template <bool CL> PT_DEV f3 get_accum(const PathState& ps) { return CL ? ps.sum : slice_get(ps); }
+
+template <bool CL> PT_DEV void set_color(PathState& ps, const f3& v)
+{
+    if (CL) slice_set(ps, v);
+    else ps.sum = v;
+}
+
+template <bool CL> PT_DEV void set_accum(PathState& ps, const f3& v)
+{
+    if (CL) ps.sum = v;
+    else slice_set(ps, v);
+}
+
+template <bool AUX, bool CL>
 PT_DEV void load_pixel(const TraceParams& P, const PixelCtx& pc, Xorwow& rng, PathState& ps, uint32_t accL)
 {
     // AUX: resume launches (see ssg_fold_kernel; pixels the fold finished are skipped by the caller)
@@ -1191,11 +1210,12 @@ PT_DEV void load_pixel(const TraceParams& P, const PixelCtx& pc, Xorwow& rng, Pa
     rng.v2 = P.rng[3 * pc.npix + pc.li];
     rng.v3 = P.rng[4 * pc.npix + pc.li];
     rng.v4 = P.rng[5 * pc.npix + pc.li];
-    ps.col = accL;
-    ps.accum = splat(0.0f);
+    ps.slot = accL;
     if (!P.ignoreFirst || (AUX && P.fold)) {     // the first call of an ignoreHistory launch overwrites it
         const float4 a = P.accum[pc.li];
-        ps.accum = mk(a.x, a.y, a.z);
+        set_accum<CL>(ps, mk(a.x, a.y, a.z));
+    } else if (CL) {
+        ps.sum = splat(0.0f);
     }
     f3 color = splat(0.0f);
     ps.L = splat(0.0f);
@@ -1211,19 +1231,20 @@ PT_DEV void load_pixel(const TraceParams& P, const PixelCtx& pc, Xorwow& rng, Pa
         ps.c = sc >> 16;
         ps.alive = ps.c < P.chunks;
     }
-    set_color(ps, color);
+    set_color<CL>(ps, color);
 }
 
 // Run-ahead (MODE 4): the previous launch's stash of this call's first k samples (same camera, scene,
 // textures, sky and RNG state: the host checked the key) -- their colour sum in sample order from 0
 // and the XORWOW state after them.  A stash longer than this call's spp cannot be split: dropped.
+template <bool CL>
 PT_DEV void ahead_load(const TraceParams& P, const PixelCtx& pc, Xorwow& rng, PathState& ps)
 {
     const uint32_t* A = P.ahead;
     const size_t n = pc.npix, li = pc.li;
     const uint32_t k = A[3 * n + li];
     if (k == 0u || k > P.spp) return;
-    set_color(ps, mk(__uint_as_float(A[li]), __uint_as_float(A[n + li]), __uint_as_float(A[2 * n + li])));
+    set_color<CL>(ps, mk(__uint_as_float(A[li]), __uint_as_float(A[n + li]), __uint_as_float(A[2 * n + li])));
     ps.s = k;
     rng.d = A[4 * n + li];
     rng.v0 = A[5 * n + li];
@@ -1233,6 +1254,7 @@ PT_DEV void ahead_load(const TraceParams& P, const PixelCtx& pc, Xorwow& rng, Pa
     rng.v4 = A[9 * n + li];
 }
 
+template <bool CL>
 PT_DEV void store_pixel(const TraceParams& P, const PixelCtx& pc, const Xorwow& rng, const PathState& ps)
 {
     // The pixel index passes through an empty asm so the store addresses are recomputed here from
@@ -1246,7 +1268,8 @@ PT_DEV void store_pixel(const TraceParams& P, const PixelCtx& pc, const Xorwow& 
     P.rng[3 * pc.npix + li] = rng.v2;
     P.rng[4 * pc.npix + li] = rng.v3;
     P.rng[5 * pc.npix + li] = rng.v4;
-    P.accum[li] = make_float4(ps.accum.x, ps.accum.y, ps.accum.z, 1.0f);   // trace.cu:198, once per launch
+    const f3 acc = get_accum<CL>(ps);
+    P.accum[li] = make_float4(acc.x, acc.y, acc.z, 1.0f);   // trace.cu:198, once per launch
 }
 
 // Run-ahead (MODE 4): after every sample of the NEXT call a lane stashes the call's colour sum so far
@@ -1280,37 +1303,37 @@ PT_DEV void ahead_store(const TraceParams& P, const PixelCtx& pc, const f3& colo
 // (trace.cu:193-198).  AHEAD: a lane already in run-ahead (ps.c == chunks) has done a whole next call:
 // it stashes it and stops; a lane finishing its last call stores its pixel now (the call's RNG state
 // and accumulation are final here) and, when the launch makes a stash, goes on with the next call.
-template <bool AHEAD>
+template <bool AHEAD, bool CL>
 PT_DEV void end_call(const TraceParams& P, const PixelCtx& pc, PathState& ps, const Xorwow& rng)
 {
-    const f3 color = get_color(ps);
+    const f3 color = get_color<CL>(ps);
     if (AHEAD && ps.c == P.chunks) {
         ahead_store(P, pc, color, ps.s, rng);
         ps.alive = false;
         return;
     }
     const bool ignore = (ps.c == 0) && P.ignoreFirst;
-    ps.accum = ignore ? color : add(color, ps.accum);
-    set_color(ps, splat(0.0f));
+    set_accum<CL>(ps, ignore ? color : add(color, get_accum<CL>(ps)));
+    set_color<CL>(ps, splat(0.0f));
     ps.s = 0;
     if (++ps.c == P.chunks) {
         ps.alive = false;
         if (AHEAD) {
-            store_pixel(P, pc, rng, ps);
+            store_pixel<CL>(P, pc, rng, ps);
             if (P.aheadMake) P.ahead[3 * pc.npix + (uint32_t)pc.li] = 0u;   // no stash until a next-call sample ends
             ps.alive = P.aheadMake != 0;
         }
     }
 }
 
-template <bool STATS, bool AHEAD = false>
+template <bool STATS, bool AHEAD, bool CL>
 PT_DEV void finish_path(const TraceParams& P, PathState& ps, Xorwow& rng, float fx, float fy, Counters& cnt,
                         const PixelCtx& pc)
 {
-    const f3 color = add(get_color(ps), ps.L);
-    set_color(ps, color);
+    const f3 color = add(get_color<CL>(ps), ps.L);
+    set_color<CL>(ps, color);
     if (STATS) cnt.samples++;
-    if (++ps.s == P.spp) end_call<AHEAD>(P, pc, ps, rng);
+    if (++ps.s == P.spp) end_call<AHEAD, CL>(P, pc, ps, rng);
     else if (AHEAD && ps.c == P.chunks) ahead_store(P, pc, color, ps.s, rng);   // a next-call sample
     if (ps.alive) {
         camera_ray(P, fx, fy, rng, ps.o, ps.d);
@@ -1615,6 +1638,9 @@ PT_DEV void run_item(const TraceParams& P, uint32_t slot, Counters& cnt)
     // next launch continues from the stash when its camera and scene are the ones it was made with
     // (host key, render_impl); otherwise the stored state is the exact one to continue from.
     constexpr bool SSG = MODE == 1, AUX = MODE == 2, STRIP = MODE == 3, AHEAD = MODE == 4;
+    // the call's colour sum in LDS (get_color): the plain six-wave launch only (measured there; the
+    // run-ahead build was 0.9 % slower with it on the reference's call loop)
+    constexpr bool CL = MINW >= 6 && MODE == 0;
     const uint32_t lane = threadIdx.x & 63u;
     const WaveLds<SL, WPB, WW> Lw = wave_lds<SL, WPB, WW>(P);
     const float4* __restrict__ nodes = Lw.nodes;
@@ -1645,10 +1671,10 @@ PT_DEV void run_item(const TraceParams& P, uint32_t slot, Counters& cnt)
         PathState ps;
         SsgLane sl;
         if (SSG) ssg_load(P, pos, grp, lane, pc.li, pc.npix, rng, ps, sl);
-        else load_pixel<AUX>(P, pc, rng, ps, accL);
+        else load_pixel<AUX, CL>(P, pc, rng, ps, accL);
         if (AHEAD && P.aheadUse) {
-            ahead_load(P, pc, rng, ps);
-            if (ps.s == P.spp) end_call<true>(P, pc, ps, rng);     // a whole call was stashed
+            ahead_load<CL>(P, pc, rng, ps);
+            if (ps.s == P.spp) end_call<true, CL>(P, pc, ps, rng);     // a whole call was stashed
         }
         float fx = (float)(int32_t)pc.px, fy = (float)(int32_t)pc.py;
         camera_ray(P, fx, fy, rng, ps.o, ps.d);
@@ -1692,7 +1718,7 @@ PT_DEV void run_item(const TraceParams& P, uint32_t slot, Counters& cnt)
                 uint64_t tS = STATS ? __builtin_amdgcn_s_memtime() : 0;
                 if (shade<STATS>(P, prims, ts.elem, ts.tMax, ps, rng, cnt)) {
                     if (SSG) ssg_finish<STATS>(P, ps, rng, fx, fy, sl, lane, pc.li, cnt);
-                    else finish_path<STATS, AHEAD>(P, ps, rng, fx, fy, cnt, pc);
+                    else finish_path<STATS, AHEAD, CL>(P, ps, rng, fx, fy, cnt, pc);
                     if (STRIP && !ps.alive && stripK + 1 < P.strip) {
                         // Strip units (launches of few samples per pixel): a lane whose pixel is done
                         // stores it and takes the same position in the unit's next tile -- the tile to
@@ -1701,10 +1727,10 @@ PT_DEV void run_item(const TraceParams& P, uint32_t slot, Counters& cnt)
                         // (their own RNG stream and accumulation value): results are unchanged.
                         const PixelCtx nx = pixel_of(P, tile + stripK + 1, lane);
                         if (nx.valid) {
-                            if (!P.discard) store_pixel(P, pc, rng, ps);   // a cost pre-pass writes nothing
+                            if (!P.discard) store_pixel<CL>(P, pc, rng, ps);   // a cost pre-pass writes nothing
                             pc = nx;
                             ++stripK;
-                            load_pixel<false>(P, pc, rng, ps, accL);
+                            load_pixel<false, CL>(P, pc, rng, ps, accL);
                             fx = (float)(int32_t)pc.px;
                             fy = (float)(int32_t)pc.py;
                             camera_ray(P, fx, fy, rng, ps.o, ps.d);
@@ -1723,7 +1749,7 @@ PT_DEV void run_item(const TraceParams& P, uint32_t slot, Counters& cnt)
             uint64_t tS = STATS ? __builtin_amdgcn_s_memtime() : 0;
             if (shade<STATS>(P, prims, e, t, ps, rng, cnt)) {
                 if (SSG) ssg_finish<STATS>(P, ps, rng, fx, fy, sl, lane, pc.li, cnt);
-                else finish_path<STATS>(P, ps, rng, fx, fy, cnt, pc);
+                else finish_path<STATS, false, CL>(P, ps, rng, fx, fy, cnt, pc);
             }
             if (STATS) wave_time(cnt.cyc_shade, tS);
         }
@@ -1736,7 +1762,7 @@ PT_DEV void run_item(const TraceParams& P, uint32_t slot, Counters& cnt)
         if (STATS) wave_time(cnt.cyc_total, tAll);
         if (SSG) P.ssgCount[(size_t)sl.logItem * 64 + lane] = sl.k;
         else if (AHEAD) {}                    // stored when its last call ended (end_call)
-        else if (!P.discard) store_pixel(P, pc, rng, ps);
+        else if (!P.discard) store_pixel<CL>(P, pc, rng, ps);
         else if (AUX && P.pairsOut)           // cost pre-pass: draw pairs per sample of this pixel
         {
             P.pairsOut[pc.li] = (float)(((rng.d - P.rng[pc.li]) * kInvWeyl) >> 1) / (float)(P.spp * P.chunks);
