@@ -1137,7 +1137,8 @@ PT_DEV bool shade(const TraceParams& P, const float4* __restrict__ prims, uint32
 struct PixelCtx {
     bool valid;
     uint32_t px, py;
-    size_t li, npix;
+    uint32_t li;      // local pixel index: contexts hold < 2^30 pixels (pt_create_banded)
+    size_t npix;      // (plane offsets k * npix + li reach past 2^32 in the 10-plane run-ahead stash)
 };
 
 PT_DEV PixelCtx pixel_of(const TraceParams& P, uint32_t tile, uint32_t lane)
