@@ -27,6 +27,7 @@ def main():
     ap.add_argument("--n", type=int, default=1, help="render one rank's share of an N-way 8-row band partition")
     ap.add_argument("--rank", type=int, default=0)
     ap.add_argument("--groups", type=int, default=1, help="sample groups: 1 = off (plain launches), 0 = automatic")
+    ap.add_argument("--ahead", type=int, default=0, help="run-ahead across launches (pt_set_run_ahead): 0 automatic, 1 off")
     ap.add_argument("--block", type=int, default=1,
                     help="launches per variant per round; with > 1 the first of each block (after a switch) is dropped")
     ap.add_argument("--check", type=int, default=1, help="assert every variant bit-identical (0 for A/B-only variants)")
@@ -38,6 +39,7 @@ def main():
     pt = (pa.Pathtracer(a.width, a.height, row_offset=a.rank, row_stride=a.n, band_rows=8) if a.n > 1
           else pa.Pathtracer(a.width, a.height))
     pt.set_sample_groups(a.groups)
+    pt.set_run_ahead(a.ahead)
     cam = pt.load_scene(a.scene)
     chunks = a.spp // 8
     ref = None
