@@ -31,7 +31,7 @@ all: $(LIB)/libpt_hip.so $(LIB)/libpt_host.so $(LIB)/pathtracer $(LIB)/fp_exhaus
 $(LIB):
 	mkdir -p $(LIB)
 
-$(LIB)/libpt_hip.so: $(SRC)/pt_kernels.hip $(SRC)/pt_math.h include/pt_hip.h | $(LIB)
+$(LIB)/libpt_hip.so: $(SRC)/pt_kernels.hip $(wildcard $(SRC)/*.h) include/pt_hip.h | $(LIB)
 	$(HIPCC) $(HIPFLAGS) -shared -o $@ $(SRC)/pt_kernels.hip -lrccl
 
 $(LIB)/libpt_host.so: $(HOST_SRCS) $(HOST_HDRS) $(LIB)/libpt_hip.so

@@ -150,9 +150,10 @@ def kernel_source_sha() -> str:
     import hashlib
     import re
     h = hashlib.sha256()
-    for f in ("pathtracercuda_amd/csrc/pt_kernels.hip", "pathtracercuda_amd/csrc/pt_math.h"):
-        if (ROOT / f).exists():          # (a build snapshot for A/Bs holds no sources)
-            h.update((ROOT / f).read_bytes())
+    src = ROOT / "pathtracercuda_amd" / "csrc"      # (a build snapshot for A/Bs holds no sources)
+    for f in [src / "pt_kernels.hip"] + sorted(src.glob("*.h")):
+        if f.exists():
+            h.update(f.read_bytes())
     for f in sorted((ROOT / "include").glob("*.h")):
         h.update(f.read_bytes())
     mk = (ROOT / "Makefile").read_text() if (ROOT / "Makefile").exists() else ""
