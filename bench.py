@@ -23,7 +23,9 @@ Scaling.  The headline is the metric's own workload at every N: strong scaling o
 1920x1080 x 1024 spp image (BASELINE.json metric "1080p 1024spp, 1/2/4/8 MI355X"), value = all
 samples / the slowest rank's step time.  At N > 1 a weak-scaling record is added beside it
 (`secondary`: every GPU keeps one C3 frame's worth of pixels, the image grows by sqrt(N) per axis),
-so both are on the driver's clock; `--scaling weak` swaps them.  At N = 1 the two coincide, and the
+so both are on the driver's clock; `--scaling weak` swaps them.  Also at N > 1: C2, C4 (the 4K x
+4096 image BASELINE tiles across 8 GPUs) and C5 on the same N GPUs, strong scaling each
+(`--configs-n 0` drops them).  At N = 1 the two coincide, and the
 secondary records are the reference's unchanged call loop on C3 (128 separate render(cam, 8, i == 0)
 calls through the drop-in Pathtracer, main.cpp:272-279), a cold one-shot C3 render (fresh context,
 cost pre-pass included), C2 and C5, each C2/C5 with its roofline and CPU baseline (`--extra ''` drops
@@ -87,6 +89,8 @@ def parse_args(argv=None):
                    help="N=1, C3: also time the reference's unchanged 128-call loop (secondary record)")
     p.add_argument("--cold", type=int, default=1,
                    help="N=1, C3: also time a cold one-shot render (fresh context, pre-pass included; secondary record)")
+    p.add_argument("--configs-n", type=int, default=1,
+                   help="N>1: also time C2, C4 and C5 on the N GPUs (strong scaling; secondary records); 2: at N=1 too (test)")
     p.add_argument("--extra", default="C5", help="N=1: secondary records after C2 (comma-separated labels; '' = none)")
     p.add_argument("--group", type=int, default=-1,
                    help="in-process device group (pt_group_*): 1 = always, 0 = never, -1 = when --gpus > 1 "
@@ -128,7 +132,10 @@ def scene_path(name: str) -> str:
             spec = importlib.util.spec_from_file_location("mss", ROOT / "tools" / "make_stress_scene.py")
             mod = importlib.util.module_from_spec(spec)
             spec.loader.exec_module(mod)
-            mod.write_scene(p, grid=317, skybox=str(ROOT / "scenes" / "skybox.hdr"))
+            # every rank of a multi-GPU run may write it: each writes its own file and renames it
+            tmp = p.with_name(f"{p.name}.{os.getpid()}.tmp")
+            mod.write_scene(tmp, grid=317, skybox=str(ROOT / "scenes" / "skybox.hdr"))
+            os.replace(tmp, p)
         return str(p)
     return str(ROOT / "scenes" / f"{name}.scene.json")
 
@@ -528,6 +535,32 @@ def main():
     if mode == "group":
         out["group_timing"] = {"kernel_ms_per_step": round(kernel_ms / args.steps, 3),
                                "gather_ms_per_step": round(gather_ms / args.steps, 3)}
+    def strong_records():
+        """C2, C4 and C5 on this run's N GPUs (strong scaling of each fixed workload)."""
+        recs = []
+        # the other BASELINE configurations on the same N GPUs, each a fixed workload (strong
+        # scaling): cornell (C2), the 4K x 4096 image BASELINE tiles across 8 GPUs (C4) and the
+        # 100k-quadric stress scene (C5)
+        for label in (("C2", "C4", "C5") if args.configs_n else ()):
+            if label == args.config:
+                continue
+            c = CONFIGS[label]
+            name = f"{label} strong scaling ({c['width']}x{c['height']} x {c['spp']} spp on {n} GPUs)"
+            try:
+                rc = Run(c, c["width"], c["height"], c["spp"], rank, n, local_rank, args.band_rows, mode)
+                stc = stats_all(rc.instrument())
+                csteps = max(args.steps, 10) if label == "C2" else min(args.steps, 2)
+                ec, kc = timed(rc, csteps, 2, local_rank, dist_on, use_torch)
+                recc = record(c, rc, ec, kc, csteps, stc, n)
+                rc.close()
+            except Exception as e:     # a secondary record never costs the headline line
+                recs.append({"label": name, "error": f"{type(e).__name__}: {e}"})
+                continue
+            recc["label"] = name
+            recc["scaling"] = "strong"
+            recs.append(recc)
+        return recs
+
     if args.secondary:
         if n == 1:
             recs = []
@@ -559,6 +592,8 @@ def main():
                 if rank == 0 and args.cpu_baseline:
                     rec2["cpu_baseline"] = cpu_baseline(args, c2, c2["width"], c2["height"])
                 recs.append(rec2)
+            if args.configs_n == 2:         # test hook: the N > 1 records' code path on one GPU
+                recs += strong_records()
             out["secondary"] = recs
         else:
             other = "strong" if args.scaling == "weak" else "weak"
@@ -574,7 +609,9 @@ def main():
             recw["label"] = (f"{args.config} weak scaling (image {Ww}x{Hw}: one {cfg['width']}x{cfg['height']} frame per GPU)"
                              if other == "weak" else f"{args.config} strong scaling (the fixed {Ww}x{Hw} image on {n} GPUs)")
             recw["scaling"] = other
-            out["secondary"] = [recw]
+            recs = [recw]
+            recs += strong_records()
+            out["secondary"] = recs
     if rank == 0 and n == 1 and args.cpu_baseline:
         out["cpu_baseline"] = cpu_baseline(args, cfg, W, H)
     if rank == 0:
