@@ -1451,19 +1451,9 @@ static int render_impl(pt_context* ctx, const pt_camera* cam, uint32_t spp, uint
             return fail(ctx, PT_ERR_STATE, "pt_set_rise_repair(0): only plain launches of variant 40 have a no-repair build");
         variant = 90;
     }
-    // Grouped launches of at most one tile per wave slot (one rank's 1080p share at N = 8) are
-    // short items whose latency sets the launch: deferred shading, which trades a lane's latency for
-    // fuller hit-shading rounds, measured bimodal there (median 57.7-62.6 ms against 57.8-58.2 ms
-    // without; at N = 4, two tiles per slot, 96.8 against 103.9), so the five-wave build runs the
-    // undeferred walk there.  The six-wave build keeps its deferred walk: at N = 8 it measured 48.9 ms
-    // against 52.9 for variant 39 and 51.5 for the undeferred walk at six waves
-    // (profiles/r05_six_waves.json).
-    if (G && ctx->variant == 0 && variant == 40) {
-        int cus = 0;
-        if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, ctx->device) == hipSuccess &&
-            (uint64_t)tiles <= (uint64_t)cus * 4 * variant_waves(variant))
-            variant = 39;
-    }
+    // (Round 3 sent grouped launches of at most one tile per wave slot to the undeferred walk, 39;
+    // measured again on the C3 N = 8 share it costs 8-10 %: 52.9 ms against 47.1 (40) and 47.8-48.9
+    // (60) with deferred shading, profiles/r05_six_waves.json.  Grouped launches keep the picked walk.)
     ctx->lastGroups = 0;
     ctx->lastVariant = variant;
     memset(ctx->groupStats, 0, sizeof(ctx->groupStats));
