@@ -1036,9 +1036,12 @@ PT_API int pt_set_skybox(pt_context* ctx, uint32_t handle)
 }
 
 // Speculative sample groups: how many groups a launch uses (0 = a plain launch).  A launch of
-// `tiles` 8x8 tiles on a chip with `resident` wave slots gets enough groups for about six work items
-// per slot (at most 8, each at least 64 samples long), and runs plain when that is fewer than 4
-// (1.5 tiles per slot or more: the cost-sorted list schedule balances well enough).
+// `tiles` 8x8 tiles on a chip with `resident` wave slots is grouped when six work items per slot
+// would take at least 4 groups (under ~1.5 tiles per slot; with more, the cost-sorted list schedule
+// balances well enough), and then gets 3.5 items per slot, at least 4 groups, at most 8, each at
+// least 64 samples long.  Measured at six waves per SIMD (profiles/r05_six_waves.json, C3 rank-0
+// shares): N = 4 G = 4 / 5 / 6 / 8 78.4 / 79.5 / 80.6 / 83.7 ms; N = 8 G = 4 / 5 / 6 / 8 46.8 / 44.5 /
+// 44.5 / 46.0 ms (the six-items rule gave 5 and 8).
 static uint32_t ssg_groups(const pt_context* ctx, int variant, uint32_t tiles, uint32_t total)
 {
     if (ctx->ssgMode == 1 || !(variant == 39 || strip_capable(variant))) return 0;
@@ -1046,10 +1049,11 @@ static uint32_t ssg_groups(const pt_context* ctx, int variant, uint32_t tiles, u
     int cus = 0;
     if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, ctx->device) != hipSuccess) return 0;
     const uint64_t resident = (uint64_t)cus * 4 * variant_waves(variant);
-    uint64_t g = (6 * resident + tiles - 1) / tiles;
-    g = std::min<uint64_t>({g, 8, total / 64});
     // measured (tools/ssg_probe.py): with 2 or 3 groups the logging, the fold and the
     // extra samples cost more than the shorter tail returns; from 4 groups on the tail wins
+    if ((6 * resident + tiles - 1) / tiles < 4) return 0;
+    uint64_t g = std::max<uint64_t>(4, (7 * resident + 2 * (uint64_t)tiles - 1) / (2 * (uint64_t)tiles));
+    g = std::min<uint64_t>({g, 8, total / 64});
     return g >= 4 ? (uint32_t)g : 0;
 }
 
