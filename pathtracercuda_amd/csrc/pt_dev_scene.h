@@ -76,6 +76,7 @@ struct TraceParams {
     uint32_t* ahead;
     uint32_t aheadUse;          // != 0: the stash was made under this launch's camera and scene: consume it
     uint32_t aheadMake;         // != 0: lanes whose pixel is done go on with the next call's samples
+    uint32_t spreadCU;          // persistent grids of CU-count multiples: the CU count (spread_slot), else 0
 };
 
 // Speculative sample groups: window of a group's start offset in which an earlier group's parse can

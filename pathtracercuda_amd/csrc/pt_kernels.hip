@@ -267,6 +267,22 @@ PT_DEV void run_item(const TraceParams& P, uint32_t slot, Counters& cnt)
 // pre-pass that also measures draw pairs per sample; 3: strip units; 4: run-ahead across render()
 // calls (run_item).  Separate instantiations keep the plain kernel's register allocation free of
 // their code.
+// First dispatch slot of wave `w` of workgroup `b` in a persistent grid of nCU x k workgroups.  The
+// hardware places workgroups 0..nCU-1 on distinct CUs (round robin over the XCDs) and a workgroup's
+// waves on distinct SIMDs, four apart (tools/hwid_probe.hip), so the slots -- positions in the cost
+// order -- are dealt one per SIMD per round, every other round in reverse: a SIMD holds one of the
+// heaviest tiles next to lighter ones of the later rounds.  A shared cursor instead hands the head to
+// whichever waves start first, which cluster on a few CUs (208 distinct SIMDs among the first 1,024
+// waves to start).  A bijection onto [0, grid x WPB); later slots come from the cursor after that range.
+template <int WPB>
+PT_DEV uint32_t spread_slot(uint32_t b, uint32_t w, uint32_t nCU)
+{
+    const uint32_t per = 4u * nCU;
+    const uint32_t r = (b / nCU) * (uint32_t)(WPB / 4) + (w >> 2);
+    const uint32_t idx = (w & 3u) * nCU + b % nCU;
+    return r * per + ((r & 1u) ? per - 1u - idx : idx);
+}
+
 template <bool STATS, int SL, int WPB, int WW, int MINW, bool PERSIST = false, int MODE = 0>
 __global__ void __launch_bounds__(WPB * 64, MINW) trace_kernel(TraceParams P)
 {
@@ -274,12 +290,16 @@ __global__ void __launch_bounds__(WPB * 64, MINW) trace_kernel(TraceParams P)
     const uint32_t wave = threadIdx.x >> 6;
     stage_scene_impl<SL, WPB, WW>(P);
     Counters cnt = {};
-    uint32_t slot = PERSIST ? wave_fetch(P.tileCursor, 1u) : __builtin_amdgcn_readfirstlane(blockIdx.x * (uint32_t)WPB + wave);
+    const bool spread = PERSIST && P.spreadCU != 0;
+    const uint32_t base = spread ? gridDim.x * (uint32_t)WPB : 0u;
+    uint32_t slot = !PERSIST ? __builtin_amdgcn_readfirstlane(blockIdx.x * (uint32_t)WPB + wave)
+                  : spread   ? spread_slot<WPB>(blockIdx.x, __builtin_amdgcn_readfirstlane(wave), P.spreadCU)
+                             : wave_fetch(P.tileCursor, 1u);
     for (;;) {
     if (slot >= P.numSlots) break;               // also the grid's spare slots past the last item
     run_item<STATS, SL, WPB, WW, MINW, PERSIST, MODE>(P, slot, cnt);
     if (!PERSIST) break;
-    slot = wave_fetch(P.tileCursor, 1u);
+    slot = base + wave_fetch(P.tileCursor, 1u);
     }
     if (PERSIST) {
         // the last wave to leave rewinds the cursor for the next launch (every wave has made its
@@ -512,15 +532,18 @@ static hipError_t launch_one(const TraceParams& P, hipStream_t stream)
             cap = std::max(cus, 1) * std::max(perCu, 1);
             resident[dev & 63].store(cap);
         }
-        if (P.occCap) {                                // tuning knob (pt_set_occupancy): fewer waves per SIMD
-            int cus = 0;
-            if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) == hipSuccess && cus > 0)
-                cap = cus * std::min(cap / cus, (int)P.occCap);
-            trace_kernel<STATS, SL, WPB, WW, MINW, PERSIST, MODE><<<(unsigned)cap, WPB * 64, lds, stream>>>(P);
-            return hipGetLastError();
-        }
-        if (blocks <= (unsigned)cap) return launch_one<STATS, SL, WPB, WW, MINW, false, MODE>(P, stream);
-        blocks = (unsigned)cap;
+        int cus = 0;
+        if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess) cus = 0;
+        if (P.occCap && cus > 0)                       // tuning knob (pt_set_occupancy): fewer waves per SIMD
+            cap = cus * std::min(cap / cus, (int)P.occCap);
+        else if (P.occCap)
+            cap = 0;
+        if (!P.occCap && blocks <= (unsigned)cap) return launch_one<STATS, SL, WPB, WW, MINW, false, MODE>(P, stream);
+        if (cap <= 0) return hipErrorInvalidValue;
+        TraceParams Q = P;                             // first slots dealt per SIMD (spread_slot)
+        Q.spreadCU = (cus > 0 && WPB % 4 == 0 && cap % cus == 0) ? (uint32_t)cus : 0u;
+        trace_kernel<STATS, SL, WPB, WW, MINW, PERSIST, MODE><<<(unsigned)cap, WPB * 64, lds, stream>>>(Q);
+        return hipGetLastError();
     }
     trace_kernel<STATS, SL, WPB, WW, MINW, PERSIST, MODE><<<blocks, WPB * 64, lds, stream>>>(P);
     return hipGetLastError();
