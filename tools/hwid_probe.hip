@@ -1,6 +1,7 @@
 // Where the hardware places the waves of a persistent trace-kernel grid: every wave records its
 // hardware ids (s_getreg HW_ID and XCC_ID) and start time, for the resident grids of the five- and
-// six-wave builds (dynamic LDS sized like theirs so the occupancy matches).  Usage on the GPU box:
+// six-wave builds (dynamic LDS sized like theirs so the occupancy matches).  Build here, run on the box:
+//   hipcc --offload-arch=gfx950 -O2 -o tools/hwid_probe tools/hwid_probe.hip
 //   tools/hwid_probe > gpurun_out/hwid.txt   (one line per wave: wpb block wave xcc se sh cu simd t)
 #include <hip/hip_runtime.h>
 #include <stdio.h>
