@@ -355,8 +355,7 @@ def timed(run, steps, warmup, local_rank, dist_on, use_torch=True):
     if not use_torch:
         # the in-process device group (main): pt_group_render / pt_group_gather return after every
         # device's stream is idle, and so does pt_render on a plain context (hipEventSynchronize),
-        # so the calls are their own barrier -- and this process must not load torch (two HIP
-        # runtimes)
+        # so the calls are their own barrier
         def barrier_sync():
             pass
     else:

@@ -6,7 +6,10 @@ pathtracercuda_amd/lib/.  There is no fallback: if they are missing the import f
 from __future__ import annotations
 
 import ctypes as C
+import importlib.util
+import os
 import pathlib
+import sys
 
 LIB_DIR = pathlib.Path(__file__).resolve().parent / "lib"
 HIP_LIB = LIB_DIR / "libpt_hip.so"
@@ -155,12 +158,62 @@ def _bind(lib: C.CDLL, table: dict) -> C.CDLL:
     return lib
 
 
+def mapped_hip_runtimes() -> list:
+    """Distinct HIP runtime files (libamdhip64*) mapped into this process, from /proc/self/maps."""
+    seen = []
+    try:
+        with open("/proc/self/maps") as f:
+            for line in f:
+                parts = line.split(None, 5)
+                if len(parts) == 6 and "/libamdhip64" in parts[5]:
+                    path = os.path.realpath(parts[5].strip())
+                    if path not in seen:
+                        seen.append(path)
+    except OSError:
+        pass
+    return seen
+
+
+def check_single_runtime() -> None:
+    """Raise PathtracerError when two HIP runtimes are mapped: two copies of the runtime in one process
+    corrupt the heap at exit ("double free or corruption", rc 134)."""
+    paths = mapped_hip_runtimes()
+    if len(paths) > 1:
+        raise PathtracerError(PT_ERR_STATE, "two HIP runtimes are mapped into this process ("
+                              + ", ".join(paths) + "); load libpt_hip.so through pathtracercuda_amd._native.hip() "
+                              "before any other HIP user, or import torch first")
+
+
+def _unify_runtime() -> None:
+    """Load the HIP runtime stack the process will use before libpt_hip.so binds one.
+
+    The torch wheel ships its own libamdhip64 / librccl / libhsa-runtime64 and resolves them by file
+    name through RPATH $ORIGIN, so a torch imported after libpt_hip.so maps a second runtime next to
+    /opt/rocm's.  Preloading the wheel's files is not enough: with the wheel's own librccl.so mapped
+    before libtorch_hip.so, the process aborts at exit ("double free or corruption", measured in this
+    container with nothing else loaded).  So when torch is importable it is imported first, which is
+    the configuration every test runs; libpt_hip.so then binds the wheel's runtime by soname
+    (libamdhip64.so.7, librccl.so.1).  Without torch the system runtime (/opt/rocm) is used.
+    """
+    if "torch" in sys.modules:
+        return
+    try:
+        spec = importlib.util.find_spec("torch")
+    except (ImportError, ValueError):
+        spec = None
+    if spec is not None:
+        import torch  # noqa: F401
+
+
 def hip() -> C.CDLL:
     global _hip
     if _hip is None:
         if not HIP_LIB.exists():
             raise RuntimeError(f"{HIP_LIB} is missing: build it with `make` (or __graft_entry__.build())")
-        _hip = _bind(C.CDLL(str(HIP_LIB), mode=C.RTLD_GLOBAL), _HIP_SYMBOLS)
+        _unify_runtime()
+        lib = C.CDLL(str(HIP_LIB), mode=C.RTLD_GLOBAL)
+        check_single_runtime()
+        _hip = _bind(lib, _HIP_SYMBOLS)
     return _hip
 
 

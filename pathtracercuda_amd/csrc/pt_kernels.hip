@@ -860,7 +860,7 @@ PT_API void pt_destroy(pt_context* ctx)
 // Host-side validation of the BVH so a malformed scene can never make the kernel read out of
 // bounds or overflow its 32-entry stack (the reference does not check, trace.cu:39).
 static int validate_scene(pt_context* ctx, const pt_bvh_node* nodes, uint32_t nn, const pt_hittable* prims, uint32_t np,
-                          uint32_t& maxDepthOut)
+                          uint32_t& maxDepthOut, std::vector<uint8_t>& reach)
 {
     for (uint32_t i = 0; i < np; ++i) {
         if (prims[i].type > 6u) return fail(ctx, PT_ERR_ARG, "pt_set_scene: invalid hittable type");
@@ -875,6 +875,7 @@ static int validate_scene(pt_context* ctx, const pt_bvh_node* nodes, uint32_t nn
         st.pop_back();
         if (i >= nn) return fail(ctx, PT_ERR_ARG, "pt_set_scene: node index out of range");
         if (++visited > nn) return fail(ctx, PT_ERR_ARG, "pt_set_scene: BVH is not a tree");
+        reach[i] = 1;
         maxDepth = std::max(maxDepth, depth);
         const uint32_t pca = nodes[i].primitive_count_axis;
         const uint32_t count = pca >> 16;
@@ -899,7 +900,10 @@ PT_API int pt_set_scene(pt_context* ctx, const pt_bvh_node* nodes, uint32_t node
     if (!ctx) return PT_ERR_ARG;
     if (node_count == 0 || prim_count == 0 || !nodes || !prims) return fail(ctx, PT_ERR_ARG, "pt_set_scene: empty scene");
     uint32_t maxDepth = 1;
-    int rc = validate_scene(ctx, nodes, node_count, prims, prim_count, maxDepth);
+    // nodes reachable from the root: only they are validated, so only they are read below (an
+    // unreachable node may hold any offset; the reference never visits it either)
+    std::vector<uint8_t> reach(node_count, 0);
+    int rc = validate_scene(ctx, nodes, node_count, prims, prim_count, maxDepth, reach);
     if (rc != PT_OK) return rc;
     std::vector<float4> hn(2 * (size_t)node_count), hp(4 * (size_t)prim_count), hm(3 * (size_t)prim_count);
     bool slabFast = true;
@@ -918,7 +922,7 @@ PT_API int pt_set_scene(pt_context* ctx, const pt_bvh_node* nodes, uint32_t node
     for (uint32_t i = 0; i < node_count; ++i) {
         const uint32_t count = nodes[i].primitive_count_axis >> 16;
         if (count == 0) rec[i] = interior++;
-        else if (count > 255) cbOk = false;
+        else if (count > 255 && reach[i]) cbOk = false;
     }
     auto word = [&](uint32_t i) {
         const uint32_t count = nodes[i].primitive_count_axis >> 16;
@@ -931,7 +935,9 @@ PT_API int pt_set_scene(pt_context* ctx, const pt_bvh_node* nodes, uint32_t node
     bool dfsOrder = true;
     for (uint32_t i = node_count; i-- > 0;) {
         const uint32_t count = nodes[i].primitive_count_axis >> 16;
-        if (count) {
+        if (!reach[i]) {
+            firstPrim[i] = lastPrim[i] = 0;
+        } else if (count) {
             firstPrim[i] = nodes[i].offset;
             lastPrim[i] = nodes[i].offset + count - 1;
         } else {
@@ -943,7 +949,7 @@ PT_API int pt_set_scene(pt_context* ctx, const pt_bvh_node* nodes, uint32_t node
     }
     std::vector<float4> hc(4 * (size_t)std::max(interior, 1u), make_float4(0.0f, 0.0f, 0.0f, 0.0f));
     for (uint32_t i = 0; cbOk && i < node_count; ++i) {
-        if (rec[i] == 0xffffffffu) continue;
+        if (rec[i] == 0xffffffffu || !reach[i]) continue;   // an unreachable record stays zero
         const pt_bvh_node& L = nodes[i + 1];
         const pt_bvh_node& R = nodes[nodes[i].offset];
         float4* q = &hc[4 * (size_t)rec[i]];

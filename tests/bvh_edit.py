@@ -114,6 +114,16 @@ def insert_orphan(nodes: Sequence[Node], p: int) -> List[Node]:
     return out
 
 
+def append_malformed_orphans(nodes: Sequence[Node]) -> List[Node]:
+    """Append unreachable nodes whose fields would index out of bounds if read: an
+    interior node with a second child far past the array, a leaf of 300 primitives past the primitive
+    array, and an interior node at the last index (its first child i + 1 does not exist).  Nothing
+    reachable from the root changes."""
+    lo, hi = nodes[0][0], nodes[0][1]
+    n = len(nodes)
+    return list(nodes) + [(lo, hi, n + 1000, 0), (lo, hi, 1 << 23, 300 << 16), (lo, hi, 1, 1 << 8)]
+
+
 def rise_pair_bvh(aabbs) -> Tuple[List[Node], List[int]]:
     """Caller BVH over scenes/rise_pair.scene.json's objects (file order: 0 dome, 1 sphere A, 2 wall B
     behind A; camera looking down -z), returns (nodes, object index of each primitive slot):

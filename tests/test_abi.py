@@ -42,3 +42,19 @@ def test_hip_library_is_gfx950(tmp_path):
     text = out.stdout + out.stderr
     assert "gfx950" in text
     assert not list(N.HIP_LIB.parent.glob(N.HIP_LIB.name + ".*")), "bundle files in the package lib/"
+
+
+@pytest.mark.parametrize("order", ["native_first", "torch_first"])
+def test_import_order_keeps_one_runtime(root, order):
+    # ADVICE/VERDICT r05: libpt_hip.so loaded before torch used to map torch's and /opt/rocm's HIP
+    # runtimes side by side and abort at exit ("double free or corruption", rc 134).  _native.hip()
+    # imports torch first, so either order ends with one runtime and a clean exit.
+    import subprocess
+    import sys
+    steps = ["from pathtracercuda_amd import _native as N", "N.hip()", "import torch"]
+    if order == "torch_first":
+        steps = [steps[2]] + steps[:2]
+    code = "\n".join(steps + ["N.check_single_runtime()", "print(len(N.mapped_hip_runtimes()))"])
+    out = subprocess.run([sys.executable, "-c", code], cwd=root, capture_output=True, text=True, timeout=300)
+    assert out.returncode == 0, out.stderr[-2000:]
+    assert out.stdout.split()[-1] == "1"

@@ -8,7 +8,6 @@ chunking).
 """
 import numpy as np
 import pytest
-import torch  # noqa: F401 -- before the native libraries: one HIP runtime per process
 
 import pathtracercuda_amd as pa
 from oracle import pyoracle as po
@@ -584,13 +583,14 @@ def test_cli_headless_outputs(gpu_available, tmp_path, scenes):
 
 def test_torchrun_unpermute_matches_row_map(gpu_available, root):
     # the one-process-per-GPU gather scatters with the native unpermute kernel (pt_unpermute_bands,
-    # the kernel pt_group_gather runs); it must place every band as global_rows() says.  torch is
-    # imported first in its own process (one HIP runtime per process)
+    # the kernel pt_group_gather runs); it must place every band as global_rows() says
+    # (own process: a torch.cuda context next to the suite's native contexts)
     import subprocess
     import sys
     code = (
-        "import torch\n"
         "from pathtracercuda_amd import _native as N\n"
+        "N.hip()\n"
+        "import torch\n"
         "from pathtracercuda_amd.distributed import global_rows, max_rows\n"
         "W = 72\n"
         "for H, world, band in ((64, 3, 8), (61, 2, 8), (37, 4, 1)):\n"
@@ -802,6 +802,15 @@ def test_orphan_node_bvh_renders_exactly(gpu_available, scenes):
         pt.set_rng_state(st)
         pt.render_raw(cam, 4, 2, True)
         assert_bitexact(pt.accum(), ref.accum, f"orphan BVH, variant {variant}")
+    # unreachable nodes whose offsets point outside the arrays (and one at the last
+    # index) are never read by the upload either; the render is unchanged
+    from bvh_edit import append_malformed_orphans
+    _set_caller_bvh(pt, osc, append_malformed_orphans(bad))
+    for variant in (0, 60, 20):
+        pt.set_kernel_variant(variant)
+        pt.set_rng_state(st)
+        pt.render_raw(cam, 4, 2, True)
+        assert_bitexact(pt.accum(), ref.accum, f"malformed orphans, variant {variant}")
 
 
 def test_forced_strip_variant_without_child_box_layout(gpu_available, scenes):
