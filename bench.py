@@ -484,9 +484,9 @@ def main():
 
     dist_on = mode == "torchrun"
     if mode != "group":
-        # torch brings its own copy of the HIP runtime (torch/lib/libamdhip64.so): it must be loaded
-        # before libpt_hip.so binds one, so that the process has a single runtime.  The device-group
-        # path needs no torch at all (its calls synchronise every device themselves) and loads none.
+        # the torchrun and single-GPU paths time with torch's events and barriers; the device-group
+        # path synchronises every device in its own calls (torch is still loaded, by _native.hip(),
+        # so the process keeps a single HIP runtime: INTEGRATION.md §4)
         import torch
         import torch.distributed as dist
     if dist_on:
@@ -534,6 +534,16 @@ def main():
     if mode == "group":
         out["group_timing"] = {"kernel_ms_per_step": round(kernel_ms / args.steps, 3),
                                "gather_ms_per_step": round(gather_ms / args.steps, 3)}
+    def all_ok(ok):
+        """Every rank's verdict on a local phase: the next phase makes collective calls,
+        so all ranks run it or none does -- a rank that failed alone must not leave the others
+        blocked in a collective, or pair their collectives with the next record's."""
+        if not dist_on:
+            return ok
+        t = torch.tensor([1 if ok else 0], dtype=torch.int32, device=f"cuda:{local_rank}")
+        dist.all_reduce(t, op=dist.ReduceOp.MIN)
+        return bool(t.item())
+
     def strong_records():
         """C2, C4 and C5 on this run's N GPUs (strong scaling of each fixed workload)."""
         recs = []
@@ -545,14 +555,27 @@ def main():
                 continue
             c = CONFIGS[label]
             name = f"{label} strong scaling ({c['width']}x{c['height']} x {c['spp']} spp on {n} GPUs)"
+            # local phase (context, scene, instrumented chunks: no collective), then one agreement
+            rc, raw, err = None, None, None
             try:
                 rc = Run(c, c["width"], c["height"], c["spp"], rank, n, local_rank, args.band_rows, mode)
-                stc = stats_all(rc.instrument())
+                raw = rc.instrument()
+            except Exception as e:     # a secondary record never costs the headline line
+                err = f"{type(e).__name__}: {e}"
+            if not all_ok(err is None):
+                if rc is not None:
+                    rc.close()
+                recs.append({"label": name, "error": err or "failed on another rank"})
+                continue
+            # collective phase: every rank is here.  (A failure inside it on one rank alone leaves
+            # the others in the step's gather until the process group's timeout.)
+            try:
+                stc = stats_all(raw)
                 csteps = max(args.steps, 10) if label == "C2" else min(args.steps, 2)
                 ec, kc = timed(rc, csteps, 2, local_rank, dist_on, use_torch)
                 recc = record(c, rc, ec, kc, csteps, stc, n)
                 rc.close()
-            except Exception as e:     # a secondary record never costs the headline line
+            except Exception as e:
                 recs.append({"label": name, "error": f"{type(e).__name__}: {e}"})
                 continue
             recc["label"] = name

@@ -338,3 +338,117 @@ PT_DEV bool traverse_cb_phase(const float4* __restrict__ cnodes, const float4* _
     ts.tMax = tMax;
     return done;
 }
+
+// ---------------------------------------------------------------------------------------------
+// Single-exit form of the resumable walk (A/B).  The same per-lane sequence of node tests, stack
+// operations, leaf tests and repairs as traverse_cb_phase; what changes is the control flow the
+// compiler sees.  There, a lane leaves the interior loop by reaching a leaf OR by an empty pop
+// (`return true` from inside the pop loop), and the phase loop by four breaks -- each extra exit is
+// an exec mask the structurizer keeps and updates with scalar instructions on every iteration
+// (~26 SALU against ~40 VALU per interior visit in the ISA of variant 60).  Here the end of the
+// traversal is a node word, kWalkDone, that no leaf or record can have (a leaf word with 255
+// primitives at offset 2^24 - 1 would end past any scene, pt_set_scene caps both), so every loop
+// has one exit condition, a property of `cur`.
+// ---------------------------------------------------------------------------------------------
+constexpr uint32_t kWalkDone = 0xffffffffu;
+
+template <bool STATS, bool ALLFAST>
+PT_DEV void walk_interior_1x(const float4* __restrict__ cnodes, uint2* stack, const SlabRay& R, uint32_t negMask,
+                             float tMin, float tMax, uint32_t& cur, uint32_t& sp, Counters& cnt)
+{
+    while ((cur >> 24) == 0u) {                       // interior record (kWalkDone >> 24 == 255)
+        if (STATS) { cnt.node_tests += 2; wave_tick(cnt.w_node); }
+        const ChildPair ch = cb_children<ALLFAST>(cnodes, cur, R, negMask, tMin, tMax);
+        stack[64u * sp] = make_uint2(ch.wF, __float_as_uint(ch.loF));
+        sp += ch.push ? 1u : 0u;
+        cur = ch.any ? ch.wNext : kWalkDone;
+        if (!ch.any) {                                // pop the next far child still hit at t_max
+            bool more = sp > 0;
+            while (more) {
+                const uint2 e = stack[64u * (--sp)];
+                const bool pass = tMax > __uint_as_float(e.y);
+                cur = pass ? e.x : cur;
+                more = !pass && sp > 0;
+            }
+        }
+    }
+}
+
+template <bool STATS, int EXITQ, bool NOREPAIR = false>
+PT_DEV bool traverse_cb_phase_1x(const float4* __restrict__ cnodes, const float4* __restrict__ prims, uint2* stack,
+                                 const TraceParams& P, f3 o, f3 d, bool fresh, TravState& ts, Counters& cnt)
+{
+    const float tMin = 0.001f;
+    SlabRay R;
+    R.o = o;
+    R.ix = rcp_rn(d.x);
+    R.iy = rcp_rn(d.y);
+    R.iz = rcp_rn(d.z);
+    R.fast = P.slabFast && __builtin_isfinite(R.ix) && __builtin_isfinite(R.iy) && __builtin_isfinite(R.iz);
+    R.ox2 = f2(o.x, o.x);
+    R.oy2 = f2(o.y, o.y);
+    R.oz2 = f2(o.z, o.z);
+    R.ix2 = f2(R.ix, R.ix);
+    R.iy2 = f2(R.iy, R.iy);
+    R.iz2 = f2(R.iz, R.iz);
+    const uint32_t negMask = (d.x < 0.0f ? 1u : 0u) | (d.y < 0.0f ? 2u : 0u) | (d.z < 0.0f ? 4u : 0u);
+    const uint32_t nAct = (uint32_t)__popcll(__ballot(1));
+    if (fresh) {
+        ts.tMax = kFltMax;
+        ts.sp = 0;
+        ts.elem = 0xffffffffu;
+        if (STATS) { cnt.node_tests++; wave_tick(cnt.w_node); }
+        float X;
+        const float lo0 = slab_lo_x(R, f2(P.rootBox[0], P.rootBox[1]), f2(P.rootBox[2], P.rootBox[3]),
+                                    f2(P.rootBox[4], P.rootBox[5]), tMin, X);
+        ts.cur = (X > lo0 && ts.tMax > lo0) ? P.rootWord : kWalkDone;
+    }
+    uint32_t sp = ts.sp, cur = ts.cur, elem = ts.elem;
+    float tMax = ts.tMax;
+    uint64_t tPhase = STATS ? __builtin_amdgcn_s_memtime() : 0;
+    const bool allFast = __ballot(!R.fast) == 0;                         // wave-uniform
+    bool go = cur != kWalkDone;
+    while (go) {
+        if (allFast) walk_interior_1x<STATS, true>(cnodes, stack, R, negMask, tMin, tMax, cur, sp, cnt);
+        else walk_interior_1x<STATS, false>(cnodes, stack, R, negMask, tMin, tMax, cur, sp, cnt);
+        if (STATS) wave_time(cnt.cyc_node, tPhase);
+        if (cur != kWalkDone) {                       // a leaf: in-order tests, repair, next pop
+            uint32_t leafOff = cur & 0xffffffu, leafCnt = cur >> 24;
+            const uint32_t leaf0 = leafOff;
+            const float tLeaf = tMax;
+            if (STATS) leaf_round_stats(prims, leafOff, leafCnt, cnt);
+            while (leafCnt > 0) {
+                if (STATS) { cnt.prim_tests++; wave_tick(cnt.w_prim); leaf_position_stats(prims, leafOff, cnt); }
+                float t;
+                if (prim_hit(prims, leafOff, o, d, tMin, tMax, t)) {
+                    tMax = t;
+                    elem = leafOff;
+                }
+                ++leafOff;
+                --leafCnt;
+            }
+            const bool rose = tMax > tLeaf;           // see traverse_cb_phase
+            if (!NOREPAIR && __ballot(rose) != 0ull && rose) {
+                repair_pending(cnodes, stack, R, negMask, tMin, P.rootWord, leaf0, sp);
+                if (STATS) cnt.repairs++;
+            }
+            if (STATS) wave_time(cnt.cyc_leaf, tPhase);
+            cur = kWalkDone;
+            bool more = sp > 0;
+            while (more) {
+                const uint2 e = stack[64u * (--sp)];
+                const bool pass = tMax > __uint_as_float(e.y);
+                cur = pass ? e.x : cur;
+                more = !pass && sp > 0;
+            }
+        }
+        // early exit once at most EXITQ/64 of the lanes that entered are still walking
+        const bool walking = cur != kWalkDone;
+        go = walking && (uint32_t)__popcll(__ballot(walking)) * 64u > nAct * (uint32_t)EXITQ;
+    }
+    ts.sp = sp;
+    ts.cur = cur;
+    ts.elem = elem;
+    ts.tMax = tMax;
+    return cur == kWalkDone;
+}

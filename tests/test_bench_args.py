@@ -60,9 +60,10 @@ def test_gpus_below_one_exits_2(capsys):
     assert "bench.py:" in capsys.readouterr().err
 
 
-def test_group_mode_never_imports_torch(root):
-    # --group 1: libpt_hip.so is loaded by the device group before any secondary record runs, so
-    # no record may reach an `import torch` (two HIP runtimes in one process)
+def test_group_mode_timing_needs_no_torch(root):
+    # --group 1: pt_group_render / pt_group_gather synchronise every device themselves, so timed()
+    # brackets them without torch's barriers or events (torch may still be loaded: _native.hip()
+    # imports it first to keep one HIP runtime)
     code = (
         "import sys, bench\n"
         "class R:\n"

@@ -548,6 +548,33 @@ def test_stress_100k_row_subset(gpu_available, tmp_path, root):
     assert np.array_equal(pt.rng_state(), ref.rng_array())
 
 
+def test_stress_100k_rises_exact_and_counted(gpu_available, tmp_path, root):
+    # the C5 check above (115 k samples) meets no rising t_max at C5's 0.66 repairs per
+    # million samples, so the repair on the deep cache-read walk (variant 46, the build C5 runs) had
+    # never met the oracle.  Every 8th row of the 1080p image at 160 spp (41 M samples; 40 spp hold
+    # none, 160 hold 5): the oracle's rise count is positive, the default launch and variant 46 are
+    # bit-exact, and the instrumented variant-46 launch repairs exactly as often as the oracle's walk
+    # raises t_max.
+    p = _stress_scene(tmp_path, root)
+    W, H, stride, spp, chunks = 1920, 1080, 8, 8, 20
+    pt, cam, ref, osc = pair(p, W, H, row_offset=3, row_stride=stride)
+    st = pt.rng_state()
+    ref.render(osc.camera, spp, True, chunks=chunks, collect_stats=True)
+    rises = int(ref.stats[7])
+    assert rises > 0, "the sample reaches no rising t_max"
+    for variant in (0, 46):
+        pt.set_kernel_variant(variant)
+        pt.set_rng_state(st)
+        pt.render_raw(cam, spp, chunks, True)
+        assert_bitexact(pt.accum(), ref.accum, f"stress 100k rises, variant {variant}")
+        assert np.array_equal(pt.rng_state(), ref.rng_array()), f"stress 100k rises, variant {variant}: RNG"
+    pt.set_kernel_variant(46)
+    pt.set_rng_state(st)
+    stats = pt.render_instrumented(cam, spp, chunks, True)
+    assert stats["repairs"] == rises, (stats["repairs"], rises)
+    assert_bitexact(pt.accum(), ref.accum, "stress 100k rises, instrumented variant 46")
+
+
 def test_cli_headless_outputs(gpu_available, tmp_path, scenes):
     # the `pathtracer` CLI (main.cpp headless path): PNG = tonemapped image flipped vertically,
     # -ohdr = accumulation / frames; the default (one launch) and -call_loop give the same files
@@ -694,13 +721,13 @@ def test_rise_repair_runs_and_is_exact_vs_oracle(gpu_available, scenes):
     ref.render(osc.camera, spp, True, chunks=chunks, collect_stats=True)
     rises = int(ref.stats[7])
     assert rises > 0
-    for variant in (0, 40, 20, 60):
+    for variant in (0, 40, 20, 60, 46):
         pt.set_kernel_variant(variant)
         pt.set_rng_state(st)
         pt.render_raw(cam, spp, chunks, True)
         assert_bitexact(pt.accum(), ref.accum, f"rise scene, variant {variant}")
         assert np.array_equal(pt.rng_state(), ref.rng_array()), f"rise scene, variant {variant}: RNG"
-    for variant in (40, 20, 60):
+    for variant in (40, 20, 60, 61, 46):
         pt.set_kernel_variant(variant)
         pt.set_rng_state(st)
         stats = pt.render_instrumented(cam, spp, chunks, True)
@@ -739,13 +766,13 @@ def test_rise_pair_needs_the_repair(gpu_available, scenes):
     N.check_ctx(N.hip().pt_set_scene(pt._ctx, _bvh_array(nodes), len(nodes),
                                      (pa.PtHittable * len(order)).from_buffer_copy(raw), len(order)), pt._ctx)
     st = pt.rng_state()
-    for variant in (0, 40, 41, 39, 20, 1, 60, 61):
+    for variant in (0, 40, 41, 39, 20, 1, 60, 61, 46):
         pt.set_kernel_variant(variant)
         pt.set_rng_state(st)
         pt.render_raw(cam, spp, chunks, True)
         assert_bitexact(pt.accum(), ref.accum, f"rise pair, variant {variant}")
         assert np.array_equal(pt.rng_state(), ref.rng_array()), f"rise pair, variant {variant}: RNG"
-    for variant in (40, 20, 60):
+    for variant in (40, 20, 60, 61, 46):
         pt.set_kernel_variant(variant)
         pt.set_rng_state(st)
         assert pt.render_instrumented(cam, spp, chunks, True)["repairs"] == rises, variant
