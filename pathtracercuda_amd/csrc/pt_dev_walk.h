@@ -132,36 +132,7 @@ PT_DEV void repair_pending(const float4* __restrict__ cnodes, uint2* stack, cons
     }
 }
 
-// The interior walk of the resumable traversal (trace.cu:66-77 per visited node): descend until a
-// leaf is reached (returns false, cur = leaf word) or the stack holds no entry that passes its
-// re-test (returns true).  Written for few exec-mask operations (the CU's one scalar unit serves
-// all its waves): ALLFAST (wave-uniform, decided by the caller) drops the per-lane exact-form
-// branch of the slab test, and the far child is written to the stack unconditionally -- the slot
-// above the top, inside the lane's column since an interior node has at most depth - 2 pending
-// entries -- with the stack pointer advanced only when the far child is to be kept (ChildPair).
-template <bool STATS, bool ALLFAST>
-PT_DEV bool walk_interior(const float4* __restrict__ cnodes, uint2* stack, const SlabRay& R, uint32_t negMask,
-                          float tMin, float tMax, uint32_t& cur, uint32_t& sp, Counters& cnt)
-{
-    while ((cur >> 24) == 0u) {
-        if (STATS) { cnt.node_tests += 2; wave_tick(cnt.w_node); }
-        const ChildPair ch = cb_children<ALLFAST>(cnodes, cur, R, negMask, tMin, tMax);
-        stack[64u * sp] = make_uint2(ch.wF, __float_as_uint(ch.loF));
-        sp += ch.push ? 1u : 0u;
-        if (ch.any) {
-            cur = ch.wNext;
-        } else {
-            bool found = false;
-            while (sp > 0) {
-                const uint2 e = stack[64u * (--sp)];
-                if (tMax > __uint_as_float(e.y)) { cur = e.x; found = true; break; }
-            }
-            if (!found) return true;
-        }
-    }
-    return false;
-}
-
+// The one-pass child-box walk (variant 20: counts the reference's node and primitive tests).
 template <bool STATS>
 PT_DEV uint32_t traverse_cb(const float4* __restrict__ cnodes, const float4* __restrict__ prims, uint2* stack,
                             const TraceParams& P, f3 o, f3 d, float& tHit, Counters& cnt)
@@ -255,106 +226,28 @@ struct TravState {
     float tMax;
 };
 
-// The interior walk is walk_interior (the lean form: wave-uniform slab-form choice, unconditional
-// far-child write).  WW = 200 + EXITQ selects this traversal.  NOREPAIR (a test-only instantiation,
-// pt_set_rise_repair) skips repair_pending: the negative control that shows a scene exercises it.
-template <bool STATS, int EXITQ, bool NOREPAIR = false>
-PT_DEV bool traverse_cb_phase(const float4* __restrict__ cnodes, const float4* __restrict__ prims, uint2* stack,
-                              const TraceParams& P, f3 o, f3 d, bool fresh, TravState& ts, Counters& cnt)
-{
-    const float tMin = 0.001f;
-    SlabRay R;
-    R.o = o;
-    R.ix = rcp_rn(d.x);
-    R.iy = rcp_rn(d.y);
-    R.iz = rcp_rn(d.z);
-    R.fast = P.slabFast && __builtin_isfinite(R.ix) && __builtin_isfinite(R.iy) && __builtin_isfinite(R.iz);
-    R.ox2 = f2(o.x, o.x);
-    R.oy2 = f2(o.y, o.y);
-    R.oz2 = f2(o.z, o.z);
-    R.ix2 = f2(R.ix, R.ix);
-    R.iy2 = f2(R.iy, R.iy);
-    R.iz2 = f2(R.iz, R.iz);
-    const uint32_t negMask = (d.x < 0.0f ? 1u : 0u) | (d.y < 0.0f ? 2u : 0u) | (d.z < 0.0f ? 4u : 0u);
-    const uint32_t nAct = (uint32_t)__popcll(__ballot(1));
-    bool done = false;
-    if (fresh) {
-        ts.tMax = kFltMax;
-        ts.sp = 0;
-        ts.elem = 0xffffffffu;
-        ts.cur = P.rootWord;
-        if (STATS) { cnt.node_tests++; wave_tick(cnt.w_node); }
-        float X;
-        const float lo0 = slab_lo_x(R, f2(P.rootBox[0], P.rootBox[1]), f2(P.rootBox[2], P.rootBox[3]),
-                                    f2(P.rootBox[4], P.rootBox[5]), tMin, X);
-        done = !(X > lo0 && ts.tMax > lo0);
-    }
-    uint32_t sp = ts.sp, cur = ts.cur, elem = ts.elem;
-    float tMax = ts.tMax;
-    auto pop = [&]() -> bool {
-        while (sp > 0) {
-            const uint2 e = stack[64u * (--sp)];
-            if (tMax > __uint_as_float(e.y)) { cur = e.x; return true; }
-        }
-        return false;
-    };
-    uint64_t tPhase = STATS ? __builtin_amdgcn_s_memtime() : 0;
-    const bool allFast = __ballot(!R.fast) == 0;                         // wave-uniform
-    while (!done) {
-        done = allFast ? walk_interior<STATS, true>(cnodes, stack, R, negMask, tMin, tMax, cur, sp, cnt)
-                       : walk_interior<STATS, false>(cnodes, stack, R, negMask, tMin, tMax, cur, sp, cnt);
-        if (STATS) wave_time(cnt.cyc_node, tPhase);
-        if (done) break;
-        uint32_t leafOff = cur & 0xffffffu, leafCnt = cur >> 24;
-        const uint32_t leaf0 = leafOff;
-        const float tLeaf = tMax;
-        if (STATS) leaf_round_stats(prims, leafOff, leafCnt, cnt);
-        while (leafCnt > 0) {
-            if (STATS) { cnt.prim_tests++; wave_tick(cnt.w_prim); leaf_position_stats(prims, leafOff, cnt); }
-            float t;
-            if (prim_hit(prims, leafOff, o, d, tMin, tMax, t)) {
-                tMax = t;
-                elem = leafOff;
-            }
-            ++leafOff;
-            --leafCnt;
-        }
-        // t_max ended the leaf above where it started (the sphere's far-root quirk, ChildPair): boxes
-        // dropped for failing an earlier, smaller t_max may pass now.  (A rise undone within the leaf
-        // needs nothing: every dropped box failed a t_max at least as large as the one left.)
-        const bool rose = tMax > tLeaf;
-        if (!NOREPAIR && __ballot(rose) != 0ull && rose) {     // rare: a uniform test first
-            repair_pending(cnodes, stack, R, negMask, tMin, P.rootWord, leaf0, sp);
-            if (STATS) cnt.repairs++;
-        }
-        if (STATS) wave_time(cnt.cyc_leaf, tPhase);
-        if (!pop()) { done = true; break; }
-        // early exit once at most EXITQ/64 of the lanes that entered are still walking
-        if ((uint32_t)__popcll(__ballot(1)) * 64u <= nAct * (uint32_t)EXITQ) break;
-    }
-    ts.sp = sp;
-    ts.cur = cur;
-    ts.elem = elem;
-    ts.tMax = tMax;
-    return done;
-}
-
-// ---------------------------------------------------------------------------------------------
-// Single-exit form of the resumable walk (A/B).  The same per-lane sequence of node tests, stack
-// operations, leaf tests and repairs as traverse_cb_phase; what changes is the control flow the
-// compiler sees.  There, a lane leaves the interior loop by reaching a leaf OR by an empty pop
-// (`return true` from inside the pop loop), and the phase loop by four breaks -- each extra exit is
-// an exec mask the structurizer keeps and updates with scalar instructions on every iteration
-// (~26 SALU against ~40 VALU per interior visit in the ISA of variant 60).  Here the end of the
-// traversal is a node word, kWalkDone, that no leaf or record can have (a leaf word with 255
-// primitives at offset 2^24 - 1 would end past any scene, pt_set_scene caps both), so every loop
-// has one exit condition, a property of `cur`.
-// ---------------------------------------------------------------------------------------------
+// The resumable walk's control flow (round 6).  Round 5's form left the interior loop by reaching a
+// leaf OR by an empty pop (`return true` from inside the pop loop), and the phase loop by four
+// breaks; each extra exit is an exec mask the structurizer keeps and updates with scalar
+// instructions on every iteration (~26 SALU against ~40 VALU per interior visit in the ISA of
+// variant 60).  Here the end of the traversal is a node word, kWalkDone, that no leaf or record can
+// have (a leaf word with 255 primitives at offset 2^24 - 1 would end past any scene, pt_set_scene
+// caps both), so every loop has one exit condition, a property of `cur` (~15 SALU per visit).  The
+// per-lane sequence of node tests, stack operations, leaf tests and repairs is unchanged.
+// Measured same-box (profiles/r06_single_exit_ab.json): C3 221.7 -> 211.7 ms (variant 60), the C4
+// N = 8 rank-2 share 486.8 -> 454.4 ms (variant 40).
+//
+// The interior walk (trace.cu:66-77 per visited node) descends until a leaf is reached or the stack
+// holds no entry that passes its re-test (cur = kWalkDone).  ALLFAST (wave-uniform, decided by the
+// caller) drops the per-lane exact-form branch of the slab test, and the far child is written to the
+// stack unconditionally -- the slot above the top, inside the lane's column since an interior node
+// has at most depth - 2 pending entries -- with the stack pointer advanced only when the far child
+// is to be kept (ChildPair).
 constexpr uint32_t kWalkDone = 0xffffffffu;
 
 template <bool STATS, bool ALLFAST>
-PT_DEV void walk_interior_1x(const float4* __restrict__ cnodes, uint2* stack, const SlabRay& R, uint32_t negMask,
-                             float tMin, float tMax, uint32_t& cur, uint32_t& sp, Counters& cnt)
+PT_DEV void walk_interior(const float4* __restrict__ cnodes, uint2* stack, const SlabRay& R, uint32_t negMask,
+                          float tMin, float tMax, uint32_t& cur, uint32_t& sp, Counters& cnt)
 {
     while ((cur >> 24) == 0u) {                       // interior record (kWalkDone >> 24 == 255)
         if (STATS) { cnt.node_tests += 2; wave_tick(cnt.w_node); }
@@ -374,9 +267,13 @@ PT_DEV void walk_interior_1x(const float4* __restrict__ cnodes, uint2* stack, co
     }
 }
 
-template <bool STATS, int EXITQ, bool NOREPAIR = false>
-PT_DEV bool traverse_cb_phase_1x(const float4* __restrict__ cnodes, const float4* __restrict__ prims, uint2* stack,
-                                 const TraceParams& P, f3 o, f3 d, bool fresh, TravState& ts, Counters& cnt)
+// WW = 200 + EXITQ selects this traversal (the wave leaves it once at most EXITQ/64 of the lanes
+// that entered still walk, see above).  NOREPAIR (a test-only instantiation, pt_set_rise_repair)
+// skips repair_pending: the negative control that shows a scene exercises it.  PRIM1X: the one-exit
+// primitive test (A/B).
+template <bool STATS, int EXITQ, bool NOREPAIR = false, bool PRIM1X = false>
+PT_DEV bool traverse_cb_phase(const float4* __restrict__ cnodes, const float4* __restrict__ prims, uint2* stack,
+                              const TraceParams& P, f3 o, f3 d, bool fresh, TravState& ts, Counters& cnt)
 {
     const float tMin = 0.001f;
     SlabRay R;
@@ -409,8 +306,8 @@ PT_DEV bool traverse_cb_phase_1x(const float4* __restrict__ cnodes, const float4
     const bool allFast = __ballot(!R.fast) == 0;                         // wave-uniform
     bool go = cur != kWalkDone;
     while (go) {
-        if (allFast) walk_interior_1x<STATS, true>(cnodes, stack, R, negMask, tMin, tMax, cur, sp, cnt);
-        else walk_interior_1x<STATS, false>(cnodes, stack, R, negMask, tMin, tMax, cur, sp, cnt);
+        if (allFast) walk_interior<STATS, true>(cnodes, stack, R, negMask, tMin, tMax, cur, sp, cnt);
+        else walk_interior<STATS, false>(cnodes, stack, R, negMask, tMin, tMax, cur, sp, cnt);
         if (STATS) wave_time(cnt.cyc_node, tPhase);
         if (cur != kWalkDone) {                       // a leaf: in-order tests, repair, next pop
             uint32_t leafOff = cur & 0xffffffu, leafCnt = cur >> 24;
@@ -420,15 +317,22 @@ PT_DEV bool traverse_cb_phase_1x(const float4* __restrict__ cnodes, const float4
             while (leafCnt > 0) {
                 if (STATS) { cnt.prim_tests++; wave_tick(cnt.w_prim); leaf_position_stats(prims, leafOff, cnt); }
                 float t;
-                if (prim_hit(prims, leafOff, o, d, tMin, tMax, t)) {
+                if (PRIM1X) {                         // one-exit primitive test, verdict applied by selects
+                    const bool h = prim_hit_rec_1x(load_prim(prims, leafOff), o, d, tMin, tMax, t);
+                    tMax = h ? t : tMax;
+                    elem = h ? leafOff : elem;
+                } else if (prim_hit(prims, leafOff, o, d, tMin, tMax, t)) {
                     tMax = t;
                     elem = leafOff;
                 }
                 ++leafOff;
                 --leafCnt;
             }
-            const bool rose = tMax > tLeaf;           // see traverse_cb_phase
-            if (!NOREPAIR && __ballot(rose) != 0ull && rose) {
+            // t_max ended the leaf above where it started (the sphere's far-root quirk, ChildPair):
+            // boxes dropped for failing an earlier, smaller t_max may pass now.  (A rise undone within
+            // the leaf needs nothing: every dropped box failed a t_max at least as large as the one left.)
+            const bool rose = tMax > tLeaf;
+            if (!NOREPAIR && __ballot(rose) != 0ull && rose) {     // rare: a uniform test first
                 repair_pending(cnodes, stack, R, negMask, tMin, P.rootWord, leaf0, sp);
                 if (STATS) cnt.repairs++;
             }
