@@ -272,69 +272,6 @@ PT_DEV bool prim_hit(const float4* __restrict__ prims, uint32_t p, f3 o, f3 d, f
     return prim_hit_rec(load_prim(prims, p), o, d, tMin, tMax, tOut);
 }
 
-// prim_hit_rec with one exit (A/B, traverse_cb_phase_1x): every rejection test of prim_hit_rec becomes
-// a term of one verdict, written as the negation of the original test so NaN operands pass or fail
-// exactly as there (a NaN disc, plane distance or coordinate passes every one of those tests in the
-// reference too, Hittable.inl:7-39,205-235,299-329).  Values the verdict rejects are never used: the
-// plane's division by d.y = 0 gives inf/NaN, a negative disc takes sqrt(0).
-PT_DEV bool prim_hit_rec_1x(const PrimRec& q, f3 o, f3 d, float tMin, float tMax, float& tOut)
-{
-    const uint32_t type = q.type;
-    const LocalRay r = to_local(q.r0, q.r1, q.r2, o, d);
-    bool ok;
-    float t;
-    if (type == DISK || type == QUAD) {
-        t = -r.o.y / r.d.y;
-        const float hx = r.o.x + r.d.x * t;
-        const float hz = r.o.z + r.d.z * t;
-        const bool out = type == QUAD ? (fabsf(hx) > 1.0f || fabsf(hz) > 1.0f) : ((hx * hx + hz * hz) >= 1.0f);
-        ok = r.d.y != 0.0f && !(t <= tMin || t > tMax) && !out;
-    } else if (type == CUBE) {
-        float lo = tMin, hi = tMax;
-        const float ox[3] = {r.o.x, r.o.y, r.o.z};
-        const float dx[3] = {r.d.x, r.d.y, r.d.z};
-#pragma unroll
-        for (int a = 0; a < 3; ++a) {
-            const float invD = rcp_rn(dx[a]);
-            float t0 = (-1.0f - ox[a]) * invD;
-            float t1 = (1.0f - ox[a]) * invD;
-            if (invD < 0.0f) { const float tmp = t0; t0 = t1; t1 = tmp; }
-            lo = t0 > lo ? t0 : lo;
-            hi = t1 < hi ? t1 : hi;
-        }
-        ok = !(hi <= lo);
-        t = lo;
-    } else {
-        const float B = (type == SPHERE) ? 1.0f : (type == CONE ? -1.0f : 0.0f);
-        const float Hc = (type == PARABOLOID) ? -1.0f : 0.0f;
-        const float J = (type == SPHERE || type == CYLINDER) ? -1.0f : 0.0f;
-        const f3 ro = r.o, rd = r.d;
-        const float a = (rd.x * rd.x + (B * rd.y) * rd.y) + rd.z * rd.z;
-        const float b = (((2.0f * ro.x) * rd.x + ((2.0f * B) * ro.y) * rd.y) + (2.0f * ro.z) * rd.z) + Hc * rd.y;
-        const float c = (((ro.x * ro.x + (B * ro.y) * ro.y) + ro.z * ro.z) + Hc * ro.y) + J;
-        const float disc = b * b - 4.0f * a * c;
-        const float rt = sqrt_rn(disc < 0.0f ? 0.0f : disc);
-        const float qq = b < 0.0f ? -0.5f * (b - rt) : -0.5f * (b + rt);
-        const float x0 = qq / a;
-        const float x1 = c / qq;
-        const float t0 = x0 > x1 ? x1 : x0;
-        const float t1 = x0 > x1 ? x0 : x1;
-        ok = !(disc < 0.0f) && !(t0 > tMax || t1 <= tMin);
-        if (type == SPHERE) {
-            t = t0 > tMin ? t0 : t1;
-        } else {
-            const float h0 = rd.y * t0 + ro.y;
-            const float h1 = rd.y * t1 + ro.y;
-            const bool v0 = t0 > tMin && t0 <= tMax && h0 >= -1.0f && h0 <= 1.0f;
-            const bool v1 = t1 > tMin && t1 <= tMax && h1 >= -1.0f && h1 <= 1.0f;
-            ok = ok && (v0 || v1);
-            t = v0 ? t0 : t1;
-        }
-    }
-    tOut = t;
-    return ok;
-}
-
 struct Counters {
     uint32_t node_tests, prim_tests, hits, sky, segments, samples;
     // wave-level executions of the same points (SIMD efficiency = lane count / (64 * wave count))

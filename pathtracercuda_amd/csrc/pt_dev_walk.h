@@ -269,9 +269,8 @@ PT_DEV void walk_interior(const float4* __restrict__ cnodes, uint2* stack, const
 
 // WW = 200 + EXITQ selects this traversal (the wave leaves it once at most EXITQ/64 of the lanes
 // that entered still walk, see above).  NOREPAIR (a test-only instantiation, pt_set_rise_repair)
-// skips repair_pending: the negative control that shows a scene exercises it.  PRIM1X: the one-exit
-// primitive test (A/B).
-template <bool STATS, int EXITQ, bool NOREPAIR = false, bool PRIM1X = false>
+// skips repair_pending: the negative control that shows a scene exercises it.
+template <bool STATS, int EXITQ, bool NOREPAIR = false>
 PT_DEV bool traverse_cb_phase(const float4* __restrict__ cnodes, const float4* __restrict__ prims, uint2* stack,
                               const TraceParams& P, f3 o, f3 d, bool fresh, TravState& ts, Counters& cnt)
 {
@@ -317,11 +316,7 @@ PT_DEV bool traverse_cb_phase(const float4* __restrict__ cnodes, const float4* _
             while (leafCnt > 0) {
                 if (STATS) { cnt.prim_tests++; wave_tick(cnt.w_prim); leaf_position_stats(prims, leafOff, cnt); }
                 float t;
-                if (PRIM1X) {                         // one-exit primitive test, verdict applied by selects
-                    const bool h = prim_hit_rec_1x(load_prim(prims, leafOff), o, d, tMin, tMax, t);
-                    tMax = h ? t : tMax;
-                    elem = h ? leafOff : elem;
-                } else if (prim_hit(prims, leafOff, o, d, tMin, tMax, t)) {
+                if (prim_hit(prims, leafOff, o, d, tMin, tMax, t)) {
                     tMax = t;
                     elem = leafOff;
                 }
