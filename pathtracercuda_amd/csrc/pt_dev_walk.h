@@ -75,22 +75,17 @@ struct ChildPair {
     float loNext, loF;          // their slab entry distances
 };
 
-// MINCMP (A/B, ALLFAST only): hit = min(X, tmc) > lo with tmc = t_max, or -inf when t_max is NaN --
-// one compare instead of two and a scalar AND.  Exact there: X and lo are never NaN in the fast form
-// (finite 1/d, ordered boxes), so min(X, t) > lo <=> X > lo && t > lo for any non-NaN t, and a NaN
-// t_max (the far-root quirk can produce one) fails every test in both forms.
-template <bool ALLFAST = false, bool MINCMP = false>
+template <bool ALLFAST = false>
 PT_DEV ChildPair cb_pair(const float4& Q0, const float4& Q1, const float4& Q2, const float4& Q3, const SlabRay& R,
-                         uint32_t negMask, float tMin, float tMax, float tmc = 0.0f)
+                         uint32_t negMask, float tMin, float tMax)
 {
     float XL, XR;
     const float loL = slab_lo_x<ALLFAST>(R, f2(Q0.x, Q0.y), f2(Q0.z, Q0.w), f2(Q1.x, Q1.y), tMin, XL);
     const float loR = slab_lo_x<ALLFAST>(R, f2(Q2.x, Q2.y), f2(Q2.z, Q2.w), f2(Q1.z, Q1.w), tMin, XR);
     const bool isNeg = (negMask & __float_as_uint(Q3.z)) != 0u;
     const uint32_t wL = __float_as_uint(Q3.x), wR = __float_as_uint(Q3.y);
-    constexpr bool MC = ALLFAST && MINCMP;
-    const bool hL = MC ? __builtin_fminf(XL, tmc) > loL : (XL > loL && tMax > loL);
-    const bool hR = MC ? __builtin_fminf(XR, tmc) > loR : (XR > loR && tMax > loR);
+    const bool hL = XL > loL && tMax > loL;
+    const bool hR = XR > loR && tMax > loR;
     const bool takeL = hL && (!hR || !isNeg);
     ChildPair c;
     c.push = hL && hR;
@@ -102,12 +97,12 @@ PT_DEV ChildPair cb_pair(const float4& Q0, const float4& Q1, const float4& Q2, c
     return c;
 }
 
-template <bool ALLFAST = false, bool MINCMP = false>
+template <bool ALLFAST = false>
 PT_DEV ChildPair cb_children(const float4* __restrict__ cnodes, uint32_t cur, const SlabRay& R, uint32_t negMask,
-                             float tMin, float tMax, float tmc = 0.0f)
+                             float tMin, float tMax)
 {
-    return cb_pair<ALLFAST, MINCMP>(cnodes[4 * cur], cnodes[4 * cur + 1], cnodes[4 * cur + 2], cnodes[4 * cur + 3], R,
-                                    negMask, tMin, tMax, tmc);
+    return cb_pair<ALLFAST>(cnodes[4 * cur], cnodes[4 * cur + 1], cnodes[4 * cur + 2], cnodes[4 * cur + 3], R, negMask,
+                            tMin, tMax);
 }
 
 // The reference's pending far children at leaf `leafOff` (after a leaf raised t_max): its stack
@@ -250,14 +245,13 @@ struct TravState {
 // is to be kept (ChildPair).
 constexpr uint32_t kWalkDone = 0xffffffffu;
 
-template <bool STATS, bool ALLFAST, int WF = 0>
+template <bool STATS, bool ALLFAST>
 PT_DEV void walk_interior(const float4* __restrict__ cnodes, uint2* stack, const SlabRay& R, uint32_t negMask,
                           float tMin, float tMax, uint32_t& cur, uint32_t& sp, Counters& cnt)
 {
-    const float tmc = tMax == tMax ? tMax : -__builtin_inff();
     while ((cur >> 24) == 0u) {                       // interior record (kWalkDone >> 24 == 255)
         if (STATS) { cnt.node_tests += 2; wave_tick(cnt.w_node); }
-        const ChildPair ch = cb_children<ALLFAST, (WF & 1) != 0>(cnodes, cur, R, negMask, tMin, tMax, tmc);
+        const ChildPair ch = cb_children<ALLFAST>(cnodes, cur, R, negMask, tMin, tMax);
         stack[64u * sp] = make_uint2(ch.wF, __float_as_uint(ch.loF));
         sp += ch.push ? 1u : 0u;
         cur = ch.any ? ch.wNext : kWalkDone;
@@ -276,7 +270,7 @@ PT_DEV void walk_interior(const float4* __restrict__ cnodes, uint2* stack, const
 // WW = 200 + EXITQ selects this traversal (the wave leaves it once at most EXITQ/64 of the lanes
 // that entered still walk, see above).  NOREPAIR (a test-only instantiation, pt_set_rise_repair)
 // skips repair_pending: the negative control that shows a scene exercises it.
-template <bool STATS, int EXITQ, bool NOREPAIR = false, int WF = 0>
+template <bool STATS, int EXITQ, bool NOREPAIR = false>
 PT_DEV bool traverse_cb_phase(const float4* __restrict__ cnodes, const float4* __restrict__ prims, uint2* stack,
                               const TraceParams& P, f3 o, f3 d, bool fresh, TravState& ts, Counters& cnt)
 {
@@ -311,8 +305,8 @@ PT_DEV bool traverse_cb_phase(const float4* __restrict__ cnodes, const float4* _
     const bool allFast = __ballot(!R.fast) == 0;                         // wave-uniform
     bool go = cur != kWalkDone;
     while (go) {
-        if (allFast) walk_interior<STATS, true, WF>(cnodes, stack, R, negMask, tMin, tMax, cur, sp, cnt);
-        else walk_interior<STATS, false, WF>(cnodes, stack, R, negMask, tMin, tMax, cur, sp, cnt);
+        if (allFast) walk_interior<STATS, true>(cnodes, stack, R, negMask, tMin, tMax, cur, sp, cnt);
+        else walk_interior<STATS, false>(cnodes, stack, R, negMask, tMin, tMax, cur, sp, cnt);
         if (STATS) wave_time(cnt.cyc_node, tPhase);
         if (cur != kWalkDone) {                       // a leaf: in-order tests, repair, next pop
             uint32_t leafOff = cur & 0xffffffu, leafCnt = cur >> 24;

@@ -167,7 +167,6 @@ PT_DEV void run_item(const TraceParams& P, uint32_t slot, Counters& cnt)
             // DEFERQ + SKYQ <= 8, so when every live lane is ready one class always runs.
             constexpr int DEFERQ = (WW / 1000) % 10, SKYQ = (WW / 10000) % 10;
             constexpr bool NOREPAIR = (WW / 100000) % 10 != 0;     // test-only (pt_set_rise_repair)
-            constexpr int WF = (WW / 1000000) % 10;                // walk flags (A/B): 1 = MINCMP (cb_pair)
             static_assert(DEFERQ + SKYQ <= 8, "a wave whose lanes are all ready must shade one class");
             bool fresh = true, held = false;
             TravState ts = {0u, 0u, 0xffffffffu, kFltMax};
@@ -176,7 +175,7 @@ PT_DEV void run_item(const TraceParams& P, uint32_t slot, Counters& cnt)
                 if (STATS && fresh && !held) { cnt.segments++; wave_tick(cnt.w_segments); }
                 bool tdone = true;
                 if (!held) {
-                    tdone = traverse_cb_phase<STATS, WW % 100, NOREPAIR, WF>(nodes, prims, reinterpret_cast<uint2*>(stack), P,
+                    tdone = traverse_cb_phase<STATS, WW % 100, NOREPAIR>(nodes, prims, reinterpret_cast<uint2*>(stack), P,
                                                                                  ps.o, ps.d, fresh, ts, cnt);
                     fresh = tdone;
                 }
@@ -591,8 +590,6 @@ static hipError_t launch_variant(int v, const TraceParams& P, hipStream_t stream
     // instrumented launch (lane utilisation, repairs) come from the kernel that is timed
     case 60: return launch_one<STATS, 1, 8, kV40Walk, 6, true, MODE>(P, stream);
     case 61: return launch_one<STATS, 0, 4, 14212, 6, true, MODE>(P, stream);
-    case 62: return launch_one<STATS, 1, 8, 1000000 + kV40Walk, 6, true, MODE>(P, stream);   // A/B: 60 + MINCMP
-    case 42: return launch_one<STATS, 1, 4, 1000000 + kV40Walk, 5, true, MODE>(P, stream);   // A/B: 40 + MINCMP
     case 90: return launch_one<false, 1, 4, 100000 + kV40Walk, 5, true, 0>(P, stream);   // test only: 40, no repair
     case 91: return launch_one<false, 2, 4, 113216, 4, true, 0>(P, stream);              // A/B only: 48, no repair
     default: return hipErrorInvalidValue;
@@ -631,7 +628,7 @@ static hipError_t launch_strip(int v, const TraceParams& P, hipStream_t stream)
 static bool strip_capable(int v) { return v == 40 || v == 41 || v == 46 || v == 60 || v == 61; }
 
 // Waves per SIMD a persistent variant is compiled for (its wave slots: CUs x 4 SIMDs x this).
-static uint32_t variant_waves(int v) { return v == 60 || v == 61 || v == 62 ? 6u : (v == 46 || v == 47 || v == 48 || v == 91) ? 4u : 5u; }
+static uint32_t variant_waves(int v) { return v == 60 || v == 61 ? 6u : (v == 46 || v == 47 || v == 48 || v == 91) ? 4u : 5u; }
 
 // Run-ahead launches (MODE 4) of the resumable persistent variants.
 static hipError_t launch_ahead(int v, const TraceParams& P, hipStream_t stream)
@@ -671,7 +668,7 @@ static uint32_t strip_tiles(const pt_context* ctx, int variant, uint32_t tiles, 
 static bool variant_shipped(int v)
 {
     return v == 0 || v == 1 || v == 4 || v == 6 || v == 20 || v == 40 || v == 41 || v == 46 || v == 47 || v == 48 || v == 39 ||
-           v == 60 || v == 61 || v == 62 || v == 42 || v == 91;   // 91: variant 48 without the rising-t_max rebuild (A/B of its cost only; not the reference's bits)
+           v == 60 || v == 61 || v == 91;   // 91: variant 48 without the rising-t_max rebuild (A/B of its cost only; not the reference's bits)
 }
 
 // Run-ahead (MODE 4): launches of kAheadMinSamples..kAheadMaxSamples samples per pixel make a stash

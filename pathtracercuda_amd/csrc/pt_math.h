@@ -163,6 +163,21 @@ PT_DEV f3 normalize(f3 v)
 {
     const float l2 = v.x * v.x + v.y * v.y + v.z * v.z;
     float inv;
+#if defined(PT_NORMALIZE_U) && PT_NORMALIZE_U
+    {   // A/B: the guard as a wave-uniform branch (see rcp_rn_u)
+        const float y = __builtin_amdgcn_rsqf(l2);
+        const float s0 = l2 * y, h = 0.5f * y;
+        const float l = __builtin_fmaf(__builtin_fmaf(-s0, s0, l2), h, s0);
+        const float r = __builtin_amdgcn_rcpf(l);
+        inv = __builtin_fmaf(__builtin_fmaf(-l, r, 1.0f), r, r);
+        const bool ok = __float_as_uint(l2) - 0x0f800000u <= 0x7f7fffffu - 0x0f800000u;
+        if (__ballot(!ok) != 0ull) {
+            const float g = rcp_rn(sqrtf(l2));
+            inv = ok ? inv : g;
+        }
+        return scale(inv, v);
+    }
+#endif
     if (__float_as_uint(l2) - 0x0f800000u <= 0x7f7fffffu - 0x0f800000u) {
         const float y = __builtin_amdgcn_rsqf(l2);
         const float s0 = l2 * y, h = 0.5f * y;
