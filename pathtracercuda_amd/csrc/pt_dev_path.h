@@ -20,7 +20,7 @@ PT_DEV Surface surface_of(const float4& r0, const float4& r1, const float4& r2, 
     float u = 0.0f, v = 0.0f;
     switch (type) {
     case SPHERE:
-        n = normalize(lp);
+        n = normalize_dom(lp);                              // a point on the unit sphere
         if (needUV) {
             const float theta = acos_sel(n.y);
             const float phi = atan2_sel(n.z, n.x);
@@ -76,7 +76,7 @@ PT_DEV Surface surface_of(const float4& r0, const float4& r1, const float4& r2, 
 PT_DEV void tangent_frame(f3 N, f3& t, f3& b)
 {
     const f3 up = fabsf(N.z) < 0.999f ? mk(0.0f, 0.0f, 1.0f) : mk(1.0f, 0.0f, 0.0f);
-    t = normalize(cross(up, N));
+    t = normalize_dom(cross(up, N));           // N unit, |up . N| < 0.999 or up = x: |up x N|^2 >= 0.001
     b = cross(N, t);
 }
 
@@ -97,8 +97,10 @@ PT_DEV f3 vndf_sample_rsc(f3 V, float r, float s, float c, float a)
     const float t1 = r * c;
     float t2 = r * s;
     const float sv = 0.5f * (1.0f + Vh.z);
-    t2 = (1.0f - sv) * sqrt_rn(1.0f - t1 * t1) + sv * t2;
-    const f3 Nh = add(add(scale(t1, T1), scale(t2, T2)), scale(sqrt_rn(clamp01(1.0f - t1 * t1 - t2 * t2)), Vh));
+    // sqrt_dom: |t1| = |r c| <= 1, so 1 - t1^2 is +0 or >= 2^-24; (1 - t1^2) - t2^2 is NaN (t2 NaN),
+    // <= 0 (clamped to +0) or >= 2^-48 (exact difference of floats >= 2^-25 where they are close)
+    t2 = (1.0f - sv) * sqrt_dom(1.0f - t1 * t1) + sv * t2;
+    const f3 Nh = add(add(scale(t1, T1), scale(t2, T2)), scale(sqrt_dom(clamp01(1.0f - t1 * t1 - t2 * t2)), Vh));
     return normalize(mk(a * Nh.x, a * Nh.y, clamp01(Nh.z)));
 }
 
@@ -115,8 +117,11 @@ PT_DEV float vndf_pdf(f3 H, f3 V, float a)    // MonteCarlo.h:104-114
 PT_DEV f3 specular_ggx(f3 F0, float NdotV, float NdotL, float NdotH, float VdotH, float a2)  // brdf.h:56-62
 {
     const float D = d_ggx(NdotH, a2);
-    float sv, sl;                                                          // brdf.h:18-24
-    sqrt2_rn((-NdotV * a2 + NdotV) * NdotV + a2, (-NdotL * a2 + NdotL) * NdotL + a2, sv, sl);
+    // brdf.h:18-24.  NdotV = |V.z| + 1e-5, so the first operand, NdotV^2 (1 - a2) + a2 with a2 in
+    // [0, 1], is NaN or >= 1e-10 (sqrt_dom); NdotL may be any value in [0, 1], so the second keeps
+    // the guarded root
+    const float sv = sqrt_dom((-NdotV * a2 + NdotV) * NdotV + a2);
+    const float sl = sqrt_rn((-NdotL * a2 + NdotL) * NdotL + a2);
     const float lv = NdotL * sv;
     const float ll = NdotV * sl;
     const float Vis = 0.5f / (lv + ll + 1e-5f);
@@ -191,7 +196,8 @@ PT_DEV bool shade(const TraceParams& P, const float4* __restrict__ prims, uint32
     f3 tg, bt;
     tangent_frame(sf.n, tg, bt);
     const f3 wo = neg(ps.d);                                                  // MonteCarlo.h:15-22
-    const f3 V = normalize(add(add(scale(wo.x, mk(tg.x, bt.x, sf.n.x)), scale(wo.y, mk(tg.y, bt.y, sf.n.y))),
+    // (normalize_dom: a unit vector in the orthonormal frame (tg, bt, n))
+    const f3 V = normalize_dom(add(add(scale(wo.x, mk(tg.x, bt.x, sf.n.x)), scale(wo.y, mk(tg.y, bt.y, sf.n.y))),
                                scale(wo.z, mk(tg.z, bt.z, sf.n.z))));
     f3 base = mk(m0.x, m0.y, m0.z);
     if (texIdx != 0) {                                                        // Material.inl:26-35
@@ -216,9 +222,11 @@ PT_DEV bool shade(const TraceParams& P, const float4* __restrict__ prims, uint32
     }
     float sn, cs;
     sincos_pos(kTwoPi * (specular ? rnd1 : rnd0), sn, cs);
-    // sqrt of the lobe's radius uniform and the cosine lobe's sin(theta) behind one range guard
-    float sq, sinTheta;
-    sqrt2_rn(specular ? rnd0 : rnd1, 1.0f - rnd1, sq, sinTheta);
+    // sqrt of the lobe's radius uniform and the cosine lobe's sin(theta) with no range guard
+    // (sqrt_dom): uniforms lie in [2^-33, 1], LAMBERT_GGX's 2 (u - 0.5) is +0 or >= 2^-23, and 1 - u is
+    // +0 or >= 2^-25
+    const float sq = sqrt_dom(specular ? rnd0 : rnd1);
+    const float sinTheta = sqrt_dom(1.0f - rnd1);
     if (mtype == 0u) {                                                        // LAMBERT (Material.inl:67-72)
         dir = mk(cs * sinTheta, sn * sinTheta, sq);                            // cosine_sample
         pdf = div_pi(dir.z);
@@ -251,8 +259,9 @@ PT_DEV bool shade(const TraceParams& P, const float4* __restrict__ prims, uint32
         }
     }
     if (killed || is_zero(att) || pdf == 0.0f) return true;                  // trace.cu:145-148
-    // Material.inl:57: normalize(tangentToWorld(...)), which itself normalizes
-    const f3 sd = normalize(normalize(add(add(scale(dir.x, tg), scale(dir.y, bt)), scale(dir.z, sf.n))));
+    // Material.inl:57: normalize(tangentToWorld(...)), which itself normalizes (normalize_dom: the
+    // sampled direction is a unit vector -- cosine sample or mirror of the unit V -- in the frame)
+    const f3 sd = normalize_dom(normalize_dom(add(add(scale(dir.x, tg), scale(dir.y, bt)), scale(dir.z, sf.n))));
     const f3 w = divs(scale(fabsf(dot(sd, sf.n)), att), pdf);                 // trace.cu:150
     ps.T = mul(ps.T, w);
     ps.o = sf.p;

@@ -55,11 +55,12 @@ PT_DEV float sqrt_rn(float x)
     return sqrtf(x);
 }
 
-// Two roots, or a root and its reciprocal, behind ONE range guard (each divergent guard costs the
-// CU's scalar unit an exec-mask save, flip and restore): when every operand is in its fast range
-// all take the fast sequences, otherwise all take rcp_rn / sqrt_rn -- the same values either way.
-// Used in shading (+0.62 % same-box); the same merge of the three ray reciprocals and of the cube
-// test's three measured -1.1 % and is not used there.
+// A root and its reciprocal behind ONE range guard (each divergent guard costs the CU's scalar unit
+// an exec-mask save, flip and restore): when the operand is in sqrt's fast range both fast
+// sequences apply, otherwise both general paths run -- the same values either way.  (Round 5 also
+// merged pairs of roots in shading this way, +0.62 %; round 6 replaced them by sqrt_dom where the
+// operand's range is known, and the merge of the three ray reciprocals and of the cube test's three
+// measured -1.1 % and is not used.)
 PT_DEV bool sqrt_fast_ok(float x) { return __float_as_uint(x) - 0x0f800000u <= 0x7f7fffffu - 0x0f800000u; }
 PT_DEV float rcp_fast(float x)
 {
@@ -72,16 +73,19 @@ PT_DEV float sqrt_fast(float x)
     const float s0 = x * y, h = 0.5f * y;
     return __builtin_fmaf(__builtin_fmaf(-s0, s0, x), h, s0);
 }
-PT_DEV void sqrt2_rn(float a, float b, float& sa, float& sb)
+// sqrt_rn for operands known to be +0, NaN or inside the fast range [2^-96, FLT_MAX] -- no range
+// guard, so no divergent region (exec-mask work on the CU's one scalar unit) and no out-of-line
+// general path.  +0 -> +0 and NaN -> the same NaN, as sqrtf returns them (its special-class select
+// passes the input through).  Callers state why the precondition holds: e.g. curand_uniform values
+// lie in [2^-33, 1], and differences of such values are 0 or at least 2^-48.
+PT_DEV float sqrt_dom(float x)
 {
-    if (sqrt_fast_ok(a) && sqrt_fast_ok(b)) {
-        sa = sqrt_fast(a);
-        sb = sqrt_fast(b);
-    } else {
-        sa = sqrt_rn(a);
-        sb = sqrt_rn(b);
-    }
+    const float y = __builtin_amdgcn_rsqf(x);
+    const float s0 = x * y, h = 0.5f * y;
+    const float s = __builtin_fmaf(__builtin_fmaf(-s0, s0, x), h, s0);
+    return x > 0.0f ? s : x;
 }
+
 // 1 / sqrt_rn(x): a root in sqrt's fast range lies in [2^-48, 2^64], inside rcp's fast range
 PT_DEV float rcp_sqrt_rn(float x)
 {
@@ -188,6 +192,21 @@ PT_DEV f3 normalize(f3 v)
         inv = rcp_rn(sqrtf(l2));
     }
     return scale(inv, v);
+}
+// normalize for vectors whose |v|^2 is NaN or inside [2^-96, FLT_MAX] (unit-length up to rounding:
+// a point on the unit sphere, a unit vector in an orthonormal frame, the cross product of the
+// up vector with a unit normal at least 0.001 away from it) -- no range guard.  A NaN |v|^2 gives
+// the same NaN as the general path: 1 / sqrtf(NaN) passes the NaN through (sqrtf's special-class
+// select, then the division's fixup of a NaN denominator).
+PT_DEV f3 normalize_dom(f3 v)
+{
+    const float l2 = v.x * v.x + v.y * v.y + v.z * v.z;
+    const float y = __builtin_amdgcn_rsqf(l2);
+    const float s0 = l2 * y, h = 0.5f * y;
+    const float l = __builtin_fmaf(__builtin_fmaf(-s0, s0, l2), h, s0);
+    const float r = __builtin_amdgcn_rcpf(l);
+    const float inv = __builtin_fmaf(__builtin_fmaf(-l, r, 1.0f), r, r);
+    return scale(l2 == l2 ? inv : l2, v);
 }
 PT_DEV f3 reflect(f3 v, f3 n) { return sub(v, scale(2.0f * dot(v, n), n)); }
 PT_DEV f3 lerp(f3 x, f3 y, float a) { return add(scale(1.0f - a, x), scale(a, y)); }
@@ -305,7 +324,9 @@ PT_DEV float asin_core_le_half(float a)                  // asin_core for 0 <= a
 PT_DEV float acos_sel(float x)
 {
     const bool lo = x < -0.5f, hi = x > 0.5f;
-    const float s = sqrt_rn(0.5f * (lo ? (1.0f + x) : (1.0f - x)));
+    // sqrt_dom: for |x| <= 1 the operand is +0 or >= 2^-26 (a multiple of ulp(x) / 2); |x| > 1 and NaN
+    // give a negative or NaN operand whose root is never used (overwritten below)
+    const float s = sqrt_dom(0.5f * (lo ? (1.0f + x) : (1.0f - x)));
     const float r = asin_core_le_half((lo || hi) ? s : fabsf(x));
     float res = lo ? kPi - 2.0f * r : (hi ? 2.0f * r : (x < 0.0f ? kPio2 + r : kPio2 - r));
     if (!(x >= -1.0f && x <= 1.0f)) res = (x != x) ? x : __uint_as_float(0x7fc00000u);

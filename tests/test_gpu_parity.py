@@ -182,7 +182,8 @@ def test_fast_reciprocal_and_sqrt_exhaustive(gpu_available, root):
     assert res["sqrt_rn"]["mismatches"] == 0, res["sqrt_rn"]
     assert res["rcp_rn_u"]["mismatches"] == 0, res["rcp_rn_u"]
     assert res["sqrt_rn_u"]["mismatches"] == 0, res["sqrt_rn_u"]
-    for k in ("acos_sel", "atan_pos_sel", "atan2_sel_y", "atan2_sel_x"):   # select forms = branchy forms
+    for k in ("acos_sel", "atan_pos_sel", "atan2_sel_y", "atan2_sel_x",   # select forms = branchy forms
+              "sqrt_dom", "nan_through_rcp_sqrt"):                         # guard-free forms on their domains
         assert res[k]["mismatches"] == 0, (k, res[k])
     # the guards matter: the raw sequences are not correctly rounded everywhere
     assert res["diag_rcp_newton_unguarded"]["mismatches"] > 0

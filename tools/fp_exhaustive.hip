@@ -10,7 +10,7 @@
 
 #include "../pathtracercuda_amd/csrc/pt_math.h"
 
-#define NSEQ 14
+#define NSEQ 16
 __device__ unsigned long long g_bad[NSEQ];
 __device__ uint32_t g_first[NSEQ][8];
 
@@ -60,6 +60,12 @@ __global__ void check(uint32_t base)
     const float h = __uint_as_float((xb * 2654435761u) ^ 0x9e3779b9u);
     check_one(12, __float_as_uint(pt::atan2_sel(x, h)) == __float_as_uint(pt::atan2_(x, h)), xb);
     check_one(13, __float_as_uint(pt::atan2_sel(h, x)) == __float_as_uint(pt::atan2_(h, x)), xb);
+    // sqrt_dom (guard-free root for operands that are +0, NaN or in [2^-96, FLT_MAX]): bit for bit,
+    // NaN payloads included, against sqrtf on that domain
+    const bool dom = xb == 0u || x != x || (xb - 0x0f800000u <= 0x7f7fffffu - 0x0f800000u);
+    check_one(14, !dom || __float_as_uint(pt::sqrt_dom(x)) == __float_as_uint(ref_sqrt), xb);
+    // normalize_dom's NaN rule: 1 / sqrtf(NaN) through the general path is that same NaN
+    check_one(15, x == x || __float_as_uint(pt::rcp_rn(sqrtf(x))) == xb, xb);
 }
 
 int main()
@@ -76,7 +82,8 @@ int main()
     if (hipMemcpyFromSymbol(first, HIP_SYMBOL(g_first), sizeof(first)) != hipSuccess) return 2;
     const char* names[NSEQ] = {"rcp_rn", "sqrt_rn", "diag_rcp_raw_all_inputs", "diag_rcp_newton_unguarded",
                                "diag_sqrt_raw_all_inputs", "diag_sqrt_rsq_newton_unguarded", "div_pi", "div_two_pi",
-                               "rcp_rn_u", "sqrt_rn_u", "acos_sel", "atan_pos_sel", "atan2_sel_y", "atan2_sel_x"};
+                               "rcp_rn_u", "sqrt_rn_u", "acos_sel", "atan_pos_sel", "atan2_sel_y", "atan2_sel_x",
+                               "sqrt_dom", "nan_through_rcp_sqrt"};
     printf("{\n  \"inputs\": 4294967296,\n");
     for (int k = 0; k < NSEQ; ++k) {
         printf("  \"%s\": {\"mismatches\": %llu, \"first\": [", names[k], bad[k]);
