@@ -75,9 +75,10 @@ PT_DEV float sqrt_fast(float x)
 }
 // sqrt_rn for operands known to be +0, NaN or inside the fast range [2^-96, FLT_MAX] -- no range
 // guard, so no divergent region (exec-mask work on the CU's one scalar unit) and no out-of-line
-// general path.  +0 -> +0 and NaN -> the same NaN, as sqrtf returns them (its special-class select
-// passes the input through).  Callers state why the precondition holds: e.g. curand_uniform values
-// lie in [2^-33, 1], and differences of such values are 0 or at least 2^-48.
+// general path.  +0 -> +0 and a quiet NaN -> the same NaN, as sqrtf returns them (its special-class
+// select passes the input through; operands computed by arithmetic are never signalling NaNs).
+// Callers state why the precondition holds: e.g. curand_uniform values lie in [2^-33, 1], and
+// differences of such values are 0 or at least 2^-48.  tools/fp_exhaustive.hip checks the domain.
 PT_DEV float sqrt_dom(float x)
 {
     const float y = __builtin_amdgcn_rsqf(x);
