@@ -206,9 +206,18 @@ PT_API int pt_read_tile_costs(pt_context *ctx, uint32_t *dst, uint32_t count);
 PT_API int pt_read_tile_idle(pt_context *ctx, uint32_t *dst, uint32_t count);
 
 /* Tuning knob for A/B measurements: 0 = automatic (default); otherwise one of the shipped
- * trace-kernel variants 1, 4, 6, 20, 39, 40, 41, 46, 47, 48, 60, 61 (traversal loop shape, deferred
- * shading, BVH staged in LDS or read through the caches, occupancy target; see pt_kernels.hip).  All variants
- * produce bit-identical results.  Other numbers return PT_ERR_ARG. */
+ * trace-kernel variants (traversal loop shape, deferred shading, BVH staged in LDS or read through
+ * the caches, occupancy target; see pt_kernels.hip).  All variants produce bit-identical results.
+ *   picked automatically (0):   60 and 40 (records in LDS, six / five waves per SIMD), 61 and 41
+ *                               (records through the caches), 46 (deep BVHs, four waves), 47 / 48
+ *                               (small grids);
+ *   fallbacks the automatic choice also uses: 4 and 6 (node-at-a-time walks for scenes outside the
+ *                               child-box encoding or whose leaves are not in DFS order);
+ *   reference / counting:       1 (the reference's control flow), 20 (counts the reference's node and
+ *                               primitive tests; the bench's algorithmic bytes);
+ *   test / A-B only:            39 (no deferred shading), 91 (48 without the rising-t_max rebuild;
+ *                               not the reference's results -- its cost A/B only).
+ * Other numbers return PT_ERR_ARG. */
 PT_API int pt_set_kernel_variant(pt_context *ctx, int variant);
 
 /* Tile dispatch order: 0 = by the measured cost of each 8x8 tile, most expensive first (default:

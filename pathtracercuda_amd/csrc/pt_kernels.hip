@@ -590,11 +590,6 @@ static hipError_t launch_variant(int v, const TraceParams& P, hipStream_t stream
     // instrumented launch (lane utilisation, repairs) come from the kernel that is timed
     case 60: return launch_one<STATS, 1, 8, kV40Walk, 6, true, MODE>(P, stream);
     case 61: return launch_one<STATS, 0, 4, 14212, 6, true, MODE>(P, stream);
-    case 62: return launch_one<STATS, 1, 8, 14208, 6, true, MODE>(P, stream);   // A/B: 60, exit <= 8/64
-    case 63: return launch_one<STATS, 1, 8, 14216, 6, true, MODE>(P, stream);   // A/B: 60, exit <= 16/64
-    case 64: return launch_one<STATS, 1, 8, 13212, 6, true, MODE>(P, stream);   // A/B: 60, hits >= 3/8
-    case 65: return launch_one<STATS, 1, 8, 15212, 6, true, MODE>(P, stream);   // A/B: 60, hits >= 5/8
-    case 66: return launch_one<STATS, 1, 8, 24212, 6, true, MODE>(P, stream);   // A/B: 60, misses >= 2/8
     case 90: return launch_one<false, 1, 4, 100000 + kV40Walk, 5, true, 0>(P, stream);   // test only: 40, no repair
     case 91: return launch_one<false, 2, 4, 113216, 4, true, 0>(P, stream);              // A/B only: 48, no repair
     default: return hipErrorInvalidValue;
@@ -633,7 +628,7 @@ static hipError_t launch_strip(int v, const TraceParams& P, hipStream_t stream)
 static bool strip_capable(int v) { return v == 40 || v == 41 || v == 46 || v == 60 || v == 61; }
 
 // Waves per SIMD a persistent variant is compiled for (its wave slots: CUs x 4 SIMDs x this).
-static uint32_t variant_waves(int v) { return (v >= 60 && v <= 66) ? 6u : (v == 46 || v == 47 || v == 48 || v == 91) ? 4u : 5u; }
+static uint32_t variant_waves(int v) { return v == 60 || v == 61 ? 6u : (v == 46 || v == 47 || v == 48 || v == 91) ? 4u : 5u; }
 
 // Run-ahead launches (MODE 4) of the resumable persistent variants.
 static hipError_t launch_ahead(int v, const TraceParams& P, hipStream_t stream)
@@ -673,7 +668,7 @@ static uint32_t strip_tiles(const pt_context* ctx, int variant, uint32_t tiles, 
 static bool variant_shipped(int v)
 {
     return v == 0 || v == 1 || v == 4 || v == 6 || v == 20 || v == 40 || v == 41 || v == 46 || v == 47 || v == 48 || v == 39 ||
-           v == 60 || v == 61 || (v >= 62 && v <= 66) || v == 91;   // 91: variant 48 without the rising-t_max rebuild (A/B of its cost only; not the reference's bits)
+           v == 60 || v == 61 || v == 91;   // 91: variant 48 without the rising-t_max rebuild (A/B of its cost only; not the reference's bits)
 }
 
 // Run-ahead (MODE 4): launches of kAheadMinSamples..kAheadMaxSamples samples per pixel make a stash
