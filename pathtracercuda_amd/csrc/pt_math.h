@@ -338,10 +338,11 @@ PT_DEV float atan_pos_sel(float x)
 {
     const bool big = x > 2.414213562373095f;
     const bool mid = !big && x > 0.4142135623730950f;
-    const float rb = -rcp_rn(x);
-    const float rm = (x - 1.0f) / (x + 1.0f);
+    // one division for both reduced ranges: -1 / x (= -rcp_rn(x): round-to-nearest is sign-symmetric)
+    // or (x - 1) / (x + 1); tools/fp_exhaustive.hip checks the result against atan_pos for all inputs
+    const float q = (big ? -1.0f : x - 1.0f) / (big ? x : x + 1.0f);
     const float y = big ? kPio2 : (mid ? kPio4 : 0.0f);
-    const float t = big ? rb : (mid ? rm : x);
+    const float t = (big || mid) ? q : x;
     const float z = t * t;
     return y + ((((8.05374449538e-2f * z - 1.38776856032E-1f) * z + 1.99777106478E-1f) * z - 3.33329491539E-1f) * z * t + t);
 }
