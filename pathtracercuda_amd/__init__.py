@@ -305,6 +305,12 @@ class Pathtracer:
         for c in self._contexts():
             N.check_ctx(N.hip().pt_set_occupancy(c, int(workgroups_per_cu)), c)
 
+    def set_quiet_heads(self, cus: int, beside: int = 2) -> None:
+        """Quiet head CUs (pt_set_quiet_heads): on `cus` CUs each SIMD runs one of the heaviest tiles
+        with at most `beside` other waves; 0 = off.  Scheduling only: results are identical."""
+        for c in self._contexts():
+            N.check_ctx(N.hip().pt_set_quiet_heads(c, int(cus), int(beside)), c)
+
     def set_issue_priority(self, mode: int, level3: int = 0, level2: int = 0, level1: int = 0) -> None:
         """Issue priority by cost-order position (pt_set_issue_priority): mode 0 automatic, 1 off,
         2 explicit (positions < level3 at priority 3, < level2 at 2, < level1 at 1).  Results are
@@ -352,6 +358,11 @@ class Pathtracer:
         return max(int(N.hip().pt_last_sample_groups(c)) for c in self._contexts())
 
     @property
+    @property
+    def last_quiet_heads(self) -> int:
+        """Quiet head CUs the last launch's main pass ran with (device 0 of a group; 0 = none)."""
+        return int(N.hip().pt_last_quiet_heads(self._contexts()[0]))
+
     def last_variant(self) -> int:
         """Trace-kernel variant of the last launch's main pass (a device group: device 0's)."""
         return int(N.hip().pt_last_variant(self._contexts()[0]))

@@ -169,6 +169,35 @@ def test_schedule_knobs_do_not_change_results(gpu_available, scenes):
         assert np.array_equal(pt.rng_state(), want_rng), (prio, occ)
 
 
+def test_quiet_heads_do_not_change_results(gpu_available, scenes):
+    # quiet head CUs (pt_set_quiet_heads): heads on their own SIMDs, waves beside them capped, the
+    # rest asleep until their head is done -- every position runs once, the bits stay the same.  The
+    # five-wave build (automatic at 2.3 tiles per six-wave slot) and the forced six- and four-wave
+    # builds; a cap that leaves no wave to wait (4 waves/SIMD, 3 beside) runs without quiet CUs.
+    W, H = 1280, 720
+    pt = pa.Pathtracer(W, H)
+    cam = pt.load_scene(scenes / "generated_scene.scene.json")
+    st = pt.rng_state()
+    pt.render(cam, 8, True, chunks=2)                 # cost order
+    pt.set_rng_state(st)
+    pt.render(cam, 4, True, chunks=3)
+    want = pt.accum().view(np.uint32).copy()
+    want_rng = pt.rng_state()
+    assert pt.last_quiet_heads == 0
+    for variant, cus, beside, applied in [(0, 64, 2, 64), (0, 64, 0, 64), (0, 256, 3, 256), (0, 1000, 1, 256),
+                                          (0, 8, 1, 8), (60, 64, 2, 64), (46, 32, 1, 32), (46, 32, 3, 0)]:
+        pt.set_kernel_variant(variant)
+        pt.set_quiet_heads(cus, beside)
+        for _ in range(2):                            # the flags are cleared for the next launch
+            pt.set_rng_state(st)
+            pt.render(cam, 4, True, chunks=3)
+            assert pt.last_quiet_heads == applied, (variant, cus, beside)
+            assert np.array_equal(pt.accum().view(np.uint32), want), (variant, cus, beside)
+            assert np.array_equal(pt.rng_state(), want_rng), (variant, cus, beside)
+    pt.set_quiet_heads(0, 0)
+    pt.set_kernel_variant(0)
+
+
 def test_fast_reciprocal_and_sqrt_exhaustive(gpu_available, root):
     # pt::rcp_rn / pt::sqrt_rn (pt_math.h) against hipcc's correctly rounded 1.0f/x and sqrtf(x)
     # for every one of the 2^32 float inputs
