@@ -305,6 +305,18 @@ class Pathtracer:
         for c in self._contexts():
             N.check_ctx(N.hip().pt_set_occupancy(c, int(workgroups_per_cu)), c)
 
+    def set_issue_priority_levels(self, l0: int = 3, l1: int = 2, l2: int = 1, l3: int = 0) -> None:
+        """Wave priority of each of the four cost-order position bands (pt_set_issue_priority_levels);
+        the default 3, 2, 1, 0 ranks the head first.  Results are identical."""
+        for c in self._contexts():
+            N.check_ctx(N.hip().pt_set_issue_priority_levels(c, int(l0), int(l1), int(l2), int(l3)), c)
+
+    def set_two_ended_queue(self, back_round: int) -> None:
+        """Waves of dealing rounds >= back_round take the cheapest tiles from the back of the cost
+        order (pt_set_two_ended_queue); 0 = off.  Results are identical."""
+        for c in self._contexts():
+            N.check_ctx(N.hip().pt_set_two_ended_queue(c, int(back_round)), c)
+
     def set_quiet_heads(self, cus: int, beside: int = 2) -> None:
         """Quiet head CUs (pt_set_quiet_heads): on `cus` CUs each SIMD runs one of the heaviest tiles
         with at most `beside` other waves; 0 = off.  Scheduling only: results are identical."""
@@ -358,11 +370,11 @@ class Pathtracer:
         return max(int(N.hip().pt_last_sample_groups(c)) for c in self._contexts())
 
     @property
-    @property
     def last_quiet_heads(self) -> int:
         """Quiet head CUs the last launch's main pass ran with (device 0 of a group; 0 = none)."""
         return int(N.hip().pt_last_quiet_heads(self._contexts()[0]))
 
+    @property
     def last_variant(self) -> int:
         """Trace-kernel variant of the last launch's main pass (a device group: device 0's)."""
         return int(N.hip().pt_last_variant(self._contexts()[0]))
@@ -421,6 +433,21 @@ class Pathtracer:
         out = np.zeros(tx * ty, dtype=np.uint32)
         N.check_ctx(N.hip().pt_read_tile_idle(self._ctx, out.ctypes.data_as(C.POINTER(C.c_uint32)), tx * ty), self._ctx)
         return out.reshape(ty, tx)
+
+    def set_tile_trace(self, enabled: bool) -> None:
+        """Record per tile the start cycle and hardware ids of the wave that ran it (diagnostics)."""
+        for c in self._contexts():
+            N.check_ctx(N.hip().pt_set_tile_trace(c, int(bool(enabled))), c)
+
+    def tile_trace(self) -> np.ndarray:
+        """Last traced launch: (tiles_y x tiles_x x 2) u32 -- start cycle (low 32 bits) and
+        XCC_ID << 16 | HW_ID (bits 0-15) of the wave that ran each tile."""
+        self._single("tile_trace")
+        tx, ty = (self.width + 7) // 8, (self.rows + 7) // 8
+        out = np.zeros(2 * tx * ty, dtype=np.uint32)
+        N.check_ctx(N.hip().pt_read_tile_trace(self._ctx, out.ctypes.data_as(C.POINTER(C.c_uint32)), 2 * tx * ty),
+                    self._ctx)
+        return out.reshape(ty, tx, 2)
 
     def copy_accum_to_device(self, dst_ptr: int, nbytes: int) -> None:
         self._single("copy_accum_to_device")

@@ -135,9 +135,12 @@ PT_DEV void run_item(const TraceParams& P, uint32_t slot, Counters& cnt)
     // end the launch.  Waves on the head of the order take issue slots first (s_setprio), the rest
     // fill the gaps.  pos is wave-uniform (an SGPR), so only one s_setprio executes.  Scheduling
     // only: results are identical.
-    if (pos < P.prio[0]) __builtin_amdgcn_s_setprio(3);
-    else if (pos < P.prio[1]) __builtin_amdgcn_s_setprio(2);
-    else if (pos < P.prio[2]) __builtin_amdgcn_s_setprio(1);
+    // The level of each band is a 2-bit field of prioVal (default 3, 2, 1, 0).
+    const uint32_t band = pos < P.prio[0] ? 0u : pos < P.prio[1] ? 1u : pos < P.prio[2] ? 2u : 3u;
+    const uint32_t level = (P.prioVal >> (2u * band)) & 3u;
+    if (level == 3u) __builtin_amdgcn_s_setprio(3);
+    else if (level == 2u) __builtin_amdgcn_s_setprio(2);
+    else if (level == 1u) __builtin_amdgcn_s_setprio(1);
     else __builtin_amdgcn_s_setprio(0);
     PixelCtx pc = pixel_of(P, tile, lane);
     const uint64_t tWave = __builtin_amdgcn_s_memtime();
@@ -251,6 +254,11 @@ PT_DEV void run_item(const TraceParams& P, uint32_t slot, Counters& cnt)
         // SSG: zeroed before the launch (idle items add ~0)
         if (SSG) atomicAdd(&P.tileCost[lin], cyc / P.ssgG);
         else P.tileCost[lin] = cyc;
+        if (P.tileTrace) {                       // schedule trace (pt_set_tile_trace): start, hardware ids
+            P.tileTrace[2 * lin] = (uint32_t)tWave;
+            P.tileTrace[2 * lin + 1] = (__builtin_amdgcn_s_getreg((31 << 11) | (0 << 6) | 20) << 16) |
+                                       (__builtin_amdgcn_s_getreg((31 << 11) | (0 << 6) | 4) & 0xffffu);
+        }
         // STRIP: the unit's cost sits at its first tile, the other tiles' entries are 0, so a sort of
         // the tile costs lists the units first (pt_render: the order of a strip launch)
         if (STRIP)
@@ -353,9 +361,24 @@ __global__ void __launch_bounds__(WPB * 64, MINW) trace_kernel(TraceParams P)
                   : quiet    ? quiet_slot<WPB>(blockIdx.x, __builtin_amdgcn_readfirstlane(wave), P.spreadCU, P.quietCU, keep, kind)
                   : spread   ? spread_slot<WPB>(blockIdx.x, __builtin_amdgcn_readfirstlane(wave), P.spreadCU)
                              : wave_fetch(P.tileCursor, 1u);
+    // two-ended queue (backRound != 0): the waves of the later rounds -- the youngest, which lose
+    // equal-priority issue arbitration to the older waves of their SIMD -- take the cheapest positions
+    // from the back of the order, the older waves the expensive ones from the front.  Every fetch
+    // first claims one of the numSlots - base positions (word 0), then its end's next one (words 2 /
+    // 3), so the two ends never overlap.
+    const bool twoEnded = spread && P.backRound != 0;
+    const bool back = twoEnded &&
+                      (blockIdx.x / P.spreadCU) * (uint32_t)(WPB / 4) + (__builtin_amdgcn_readfirstlane(wave) >> 2) >= P.backRound;
+    auto next = [&]() -> uint32_t {
+        if (twoEnded) {
+            if (base + wave_fetch(P.tileCursor, 1u) >= P.numSlots) return P.numSlots;
+            return back ? P.numSlots - 1u - wave_fetch(P.tileCursor + 2, 1u) : base + wave_fetch(P.tileCursor + 3, 1u);
+        }
+        return base + wave_fetch(P.tileCursor, 1u);
+    };
     if (quiet && kind == 2) {
         quiet_wait(quiet_flag<WPB>(P));
-        slot = base + wave_fetch(P.tileCursor, 1u);
+        slot = next();
     }
     for (;;) {
     if (slot >= P.numSlots) break;               // also the grid's spare slots past the last item
@@ -365,7 +388,7 @@ __global__ void __launch_bounds__(WPB * 64, MINW) trace_kernel(TraceParams P)
     if (head && lane == 0)                       // the head tile is done: its SIMD's waiting waves go on
         __hip_atomic_store(quiet_flag<WPB>(P), 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     if (!PERSIST) break;
-    slot = base + wave_fetch(P.tileCursor, 1u);
+    slot = next();
     }
     if (quiet && slot < 4u * P.quietCU && lane == 0)   // a head position past the last item
         __hip_atomic_store(quiet_flag<WPB>(P), 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
@@ -376,10 +399,7 @@ __global__ void __launch_bounds__(WPB * 64, MINW) trace_kernel(TraceParams P)
         if (wave_fetch(P.tileCursor + 1, 1u) == gridDim.x * (uint32_t)WPB - 1) {
             if (quiet)
                 for (uint32_t i = lane; i < 4u * P.quietCU; i += 64u) P.quietFlag[i] = 0u;
-            if (lane == 0) {
-                P.tileCursor[0] = 0;
-                P.tileCursor[1] = 0;
-            }
+            if (lane < kCursorWords) P.tileCursor[lane] = 0;
         }
     }
     flush_counters<STATS>(P, cnt);
@@ -484,6 +504,9 @@ struct pt_context {
     // tile scheduling: per-tile cost of the last launch and the cost-sorted dispatch order
     uint32_t* tileCost = nullptr;
     uint32_t* tileIdle = nullptr;     // instrumented launches: per-tile mean lane idle cycles (pt_read_tile_idle)
+    uint32_t* tileTrace = nullptr;    // pt_set_tile_trace: per tile {start cycles, hardware ids} of the last launch
+    bool traceTiles = false;
+    uint32_t traceCap = 0;
     uint32_t* order = nullptr;
     uint32_t* rowMajor = nullptr;     // the row-major order (packed coordinates), before costs are known
     uint32_t* tileCursor = nullptr;   // persistent variants
@@ -505,6 +528,8 @@ struct pt_context {
     uint32_t quietCUs = 0;        // quiet head CUs (pt_set_quiet_heads; 0 = off) and the waves beside each head
     uint32_t quietCap = 0;
     uint32_t lastQuiet = 0;       // quiet head CUs the last launch ran with
+    uint32_t backRound = 0;       // pt_set_two_ended_queue: first round of waves taking from the back (0 = off)
+    uint32_t prioLevels = kPrioLevels;    // pt_set_issue_priority_levels: the level of each position band
     int prioMode = 0;             // issue priority: 0 = automatic, 1 = off, 2 = explicit bounds prioBounds
     uint32_t prioBounds[3] = {0, 0, 0};
     // speculative sample groups
@@ -910,6 +935,7 @@ PT_API void pt_destroy(pt_context* ctx)
     (void)hipFree(ctx->cnodes);
     (void)hipFree(ctx->tileCost);
     (void)hipFree(ctx->tileIdle);
+    (void)hipFree(ctx->tileTrace);
     (void)hipFree(ctx->order);
     (void)hipFree(ctx->rowMajor);
     (void)hipFree(ctx->unitMajor);
@@ -1522,13 +1548,15 @@ static int render_impl(pt_context* ctx, const pt_camera* cam, uint32_t spp, uint
     P.tileCost = sorted ? ctx->tileCost : nullptr;
     P.scatterWaves = ctx->schedule == 2 ? (uint32_t)(((size_t)ctx->rows * ctx->width + 63) / 64) : 0u;
     if (P.scatterWaves) P.order = nullptr;          // scattered mapping: slot = wave index
-    if (!ctx->tileCursor) {                         // {cursor, waves out}, then the quiet flags
-        PT_HIP_CHECK(ctx, hipMalloc(&ctx->tileCursor, (2 + kQuietWords) * sizeof(uint32_t)));
-        PT_HIP_CHECK(ctx, hipMemset(ctx->tileCursor, 0, (2 + kQuietWords) * sizeof(uint32_t)));
+    if (!ctx->tileCursor) {                         // {cursor, waves out, back, front}, then the quiet flags
+        PT_HIP_CHECK(ctx, hipMalloc(&ctx->tileCursor, (kCursorWords + kQuietWords) * sizeof(uint32_t)));
+        PT_HIP_CHECK(ctx, hipMemset(ctx->tileCursor, 0, (kCursorWords + kQuietWords) * sizeof(uint32_t)));
     }
     P.tileCursor = ctx->tileCursor;
     P.numSlots = units;
     P.occCap = ctx->occupancy;
+    P.backRound = ctx->backRound;
+    P.prioVal = ctx->prioLevels;
     // Issue priority follows the order position, so it is meaningful only on a current cost order.
     // A launch whose tile costs will rebuild the order (stale order, or this launch measures >= 4x
     // the samples the order came from; see the rebuild below) runs without it: graded priority
@@ -1537,6 +1565,17 @@ static int render_impl(pt_context* ctx, const pt_camera* cam, uint32_t spp, uint
     const bool rebuilds = ctx->schedule == 0 &&
                           (ctx->orderStale || !ctx->orderValid || (uint64_t)spp * chunks >= 4 * ctx->orderSamples);
     if (!rebuilds || ctx->prioMode == 2) issue_priority(ctx, units, P.prio);   // explicit bounds: always
+    if (ctx->traceTiles && P.tileCost) {
+        if (ctx->tileTrace && ctx->traceCap < tiles) {
+            (void)hipFree(ctx->tileTrace);
+            ctx->tileTrace = nullptr;
+        }
+        if (!ctx->tileTrace) {
+            PT_HIP_CHECK(ctx, hipMalloc(&ctx->tileTrace, 2 * (size_t)tiles * sizeof(uint32_t)));
+            ctx->traceCap = tiles;
+        }
+        P.tileTrace = ctx->tileTrace;
+    }
     if (stats) {
         PT_HIP_CHECK(ctx, hipMemsetAsync(ctx->stats, 0, kStatWords * sizeof(unsigned long long), ctx->stream));
         if (!ctx->tileIdle) PT_HIP_CHECK(ctx, hipMalloc(&ctx->tileIdle, (size_t)tiles * sizeof(uint32_t)));
@@ -1655,7 +1694,7 @@ static int render_impl(pt_context* ctx, const pt_camera* cam, uint32_t spp, uint
     if (!G && K == 1 && !ahead && !cold && !rebuilds && ctx->quietCUs) {
         P.quietCU = ctx->quietCUs;
         P.quietCap = ctx->quietCap;
-        P.quietFlag = ctx->tileCursor + 2;
+        P.quietFlag = ctx->tileCursor + kCursorWords;
     }
     tl_quietApplied = 0;
     if (G && P.tileCost) PT_HIP_CHECK(ctx, hipMemsetAsync(P.tileCost, 0, (size_t)tiles * sizeof(uint32_t), ctx->stream));
@@ -1827,9 +1866,23 @@ PT_API int pt_set_quiet_heads(pt_context* ctx, uint32_t cus, uint32_t beside)
     return PT_OK;
 }
 
+PT_API int pt_set_two_ended_queue(pt_context* ctx, uint32_t back_round)
+{
+    if (!ctx || back_round > 64) return PT_ERR_ARG;
+    ctx->backRound = back_round;
+    return PT_OK;
+}
+
 PT_API int pt_last_quiet_heads(const pt_context* ctx)
 {
     return ctx ? (int)ctx->lastQuiet : PT_ERR_ARG;
+}
+
+PT_API int pt_set_issue_priority_levels(pt_context* ctx, uint32_t l0, uint32_t l1, uint32_t l2, uint32_t l3)
+{
+    if (!ctx || l0 > 3 || l1 > 3 || l2 > 3 || l3 > 3) return PT_ERR_ARG;
+    ctx->prioLevels = l0 | l1 << 2 | l2 << 4 | l3 << 6;
+    return PT_OK;
 }
 
 PT_API int pt_set_occupancy(pt_context* ctx, uint32_t workgroups_per_cu)
@@ -1954,6 +2007,24 @@ PT_API int pt_read_tile_idle(pt_context* ctx, uint32_t* dst, uint32_t count)
     PT_HIP_CHECK(ctx, hipSetDevice(ctx->device));
     PT_HIP_CHECK(ctx, hipStreamSynchronize(ctx->stream));
     PT_HIP_CHECK(ctx, hipMemcpy(dst, ctx->tileIdle, (size_t)count * sizeof(uint32_t), hipMemcpyDeviceToHost));
+    return PT_OK;
+}
+
+PT_API int pt_set_tile_trace(pt_context* ctx, int enabled)
+{
+    if (!ctx) return PT_ERR_ARG;
+    ctx->traceTiles = enabled != 0;
+    return PT_OK;
+}
+
+PT_API int pt_read_tile_trace(pt_context* ctx, uint32_t* dst, uint32_t count)
+{
+    if (!ctx || !dst) return PT_ERR_ARG;
+    if (!ctx->tileTrace || count != 2 * ctx->orderTiles || ctx->traceCap < ctx->orderTiles)
+        return fail(ctx, PT_ERR_STATE, "pt_read_tile_trace: no traced launch of that size");
+    PT_HIP_CHECK(ctx, hipSetDevice(ctx->device));
+    PT_HIP_CHECK(ctx, hipStreamSynchronize(ctx->stream));
+    PT_HIP_CHECK(ctx, hipMemcpy(dst, ctx->tileTrace, (size_t)count * sizeof(uint32_t), hipMemcpyDeviceToHost));
     return PT_OK;
 }
 
