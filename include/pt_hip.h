@@ -237,18 +237,6 @@ PT_API int pt_set_schedule(pt_context *ctx, int mode);
  * fit, the default).  Results are identical. */
 PT_API int pt_set_occupancy(pt_context *ctx, uint32_t workgroups_per_cu);
 
-/* Quiet head CUs (chain-bound launches, e.g. a multi-GPU share): on `cus` CUs each SIMD runs one of
- * the 4 x cus heaviest tiles of the cost order with at most `beside` other waves; the SIMD's other
- * waves sleep until that tile is done.  cus = 0: off (the default).  Applies to plain launches on a
- * current cost order.  Results are identical. */
-PT_API int pt_set_quiet_heads(pt_context *ctx, uint32_t cus, uint32_t beside);
-/* Two-ended dispatch queue of persistent grids: waves of dealing rounds >= back_round (the youngest,
- * which lose equal-priority issue arbitration to their SIMD's older waves) take the cheapest tiles
- * from the back of the cost order, the others the most expensive from the front.  0 = off (default).
- * Results are identical. */
-PT_API int pt_set_two_ended_queue(pt_context *ctx, uint32_t back_round);
-/* Quiet head CUs the last launch's main pass ran with (0: none). */
-PT_API int pt_last_quiet_heads(const pt_context *ctx);
 
 /* Issue priority by position in the cost order (s_setprio): mode 0 = automatic (default), 1 = off,
  * 2 = explicit -- positions < level3 run at wave priority 3, < level2 at 2, < level1 at 1, the

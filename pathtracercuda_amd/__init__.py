@@ -311,18 +311,6 @@ class Pathtracer:
         for c in self._contexts():
             N.check_ctx(N.hip().pt_set_issue_priority_levels(c, int(l0), int(l1), int(l2), int(l3)), c)
 
-    def set_two_ended_queue(self, back_round: int) -> None:
-        """Waves of dealing rounds >= back_round take the cheapest tiles from the back of the cost
-        order (pt_set_two_ended_queue); 0 = off.  Results are identical."""
-        for c in self._contexts():
-            N.check_ctx(N.hip().pt_set_two_ended_queue(c, int(back_round)), c)
-
-    def set_quiet_heads(self, cus: int, beside: int = 2) -> None:
-        """Quiet head CUs (pt_set_quiet_heads): on `cus` CUs each SIMD runs one of the heaviest tiles
-        with at most `beside` other waves; 0 = off.  Scheduling only: results are identical."""
-        for c in self._contexts():
-            N.check_ctx(N.hip().pt_set_quiet_heads(c, int(cus), int(beside)), c)
-
     def set_issue_priority(self, mode: int, level3: int = 0, level2: int = 0, level1: int = 0) -> None:
         """Issue priority by cost-order position (pt_set_issue_priority): mode 0 automatic, 1 off,
         2 explicit (positions < level3 at priority 3, < level2 at 2, < level1 at 1).  Results are
@@ -368,11 +356,6 @@ class Pathtracer:
     def last_sample_groups(self) -> int:
         """Groups of the last launch (a device group: the largest over its devices)."""
         return max(int(N.hip().pt_last_sample_groups(c)) for c in self._contexts())
-
-    @property
-    def last_quiet_heads(self) -> int:
-        """Quiet head CUs the last launch's main pass ran with (device 0 of a group; 0 = none)."""
-        return int(N.hip().pt_last_quiet_heads(self._contexts()[0]))
 
     @property
     def last_variant(self) -> int:

@@ -83,12 +83,9 @@ _HIP_SYMBOLS = {
                                      C.c_uint32]),
     "pt_set_kernel_variant": (C.c_int, [C.c_void_p, C.c_int]),
     "pt_set_occupancy": (C.c_int, [C.c_void_p, C.c_uint32]),
-    "pt_set_quiet_heads": (C.c_int, [C.c_void_p, C.c_uint32, C.c_uint32]),
     "pt_set_tile_trace": (C.c_int, [C.c_void_p, C.c_int]),
-    "pt_set_two_ended_queue": (C.c_int, [C.c_void_p, C.c_uint32]),
     "pt_set_issue_priority_levels": (C.c_int, [C.c_void_p, C.c_uint32, C.c_uint32, C.c_uint32, C.c_uint32]),
     "pt_read_tile_trace": (C.c_int, [C.c_void_p, P(C.c_uint32), C.c_uint32]),
-    "pt_last_quiet_heads": (C.c_int, [C.c_void_p]),
     "pt_set_issue_priority": (C.c_int, [C.c_void_p, C.c_int, C.c_uint32, C.c_uint32, C.c_uint32]),
     "pt_set_schedule": (C.c_int, [C.c_void_p, C.c_int]),
     "pt_set_sample_groups": (C.c_int, [C.c_void_p, C.c_int]),

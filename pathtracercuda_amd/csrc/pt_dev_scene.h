@@ -79,17 +79,10 @@ struct TraceParams {
     uint32_t aheadUse;          // != 0: the stash was made under this launch's camera and scene: consume it
     uint32_t aheadMake;         // != 0: lanes whose pixel is done go on with the next call's samples
     uint32_t spreadCU;          // persistent grids of CU-count multiples: the CU count (spread_slot), else 0
-    // Quiet head CUs (quiet_slot; 0 = off): on the first quietCU CUs of a spread grid each SIMD runs one
-    // of the 4 x quietCU heaviest tiles with at most quietCap waves beside it; the SIMD's other waves
-    // sleep until that tile is done (quietFlag[4 x CU + SIMD] != 0), then take tiles from the cursor.
-    uint32_t quietCU;
-    uint32_t quietCap;
-    uint32_t* quietFlag;        // [4 x CUs] words, zero between launches (the last wave out clears them)
-    uint32_t backRound;         // spread grids: waves of rounds >= backRound take from the back of the order (0 = off)
+    uint32_t prioDealt;         // host only: persistent grids raise the first band to every position dealt
+                                // at the start (launch_one; automatic priority)
 };
-constexpr uint32_t kCursorWords = 4;      // tileCursor: {positions claimed, waves out, back taken, front taken}
-constexpr uint32_t kQuietWords = 4096;
-constexpr uint32_t kPrioLevels = 3u | 2u << 2 | 1u << 4 | 0u << 6;    // quietFlag capacity: 4 SIMDs x 1,024 CUs
+constexpr uint32_t kPrioLevels = 3u | 2u << 2 | 1u << 4 | 0u << 6;    // default band levels 3, 2, 1, 0
 
 // Speculative sample groups: window of a group's start offset in which an earlier group's parse can
 // join it (draw pairs; 16 x 64-bit words per lane), and the fold state kept per pixel between rounds.

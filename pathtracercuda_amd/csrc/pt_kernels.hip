@@ -291,57 +291,6 @@ PT_DEV uint32_t spread_slot(uint32_t b, uint32_t w, uint32_t nCU)
     return r * per + ((r & 1u) ? per - 1u - idx : idx);
 }
 
-// Quiet head CUs.  A chain-bound launch (few tiles per wave slot: a multi-GPU share) ends with its
-// heaviest tiles' serial sample chains, and such a chain runs 2-3x slower beside five or six other
-// waves than with one or two (tools/occupancy_probe.py, profiles/r03_occupancy_probe.json) while a
-// whole grid at low occupancy loses throughput.  So only the first hc CUs are made quiet: their
-// round-0 waves take the 4 x hc heaviest positions (one per SIMD), at most keep - 1 further rounds
-// of waves run beside them, and the waves of the later rounds sleep until the head tile of their
-// SIMD is done (quiet_wait) and then take tiles from the cursor.  The other CUs are dealt as by
-// spread_slot; the dealt positions are a bijection onto [0, quiet_base).  kind: 0 = dealt, 1 = a head
-// (dealt), 2 = waits (no slot).  Scheduling only: every position is run exactly once either way.
-template <int WPB>
-PT_DEV uint32_t quiet_slot(uint32_t b, uint32_t w, uint32_t nCU, uint32_t hc, uint32_t keep, uint32_t& kind)
-{
-    const uint32_t per = 4u * nCU, rest = nCU - hc, per2 = 4u * rest;
-    const uint32_t r = (b / nCU) * (uint32_t)(WPB / 4) + (w >> 2);
-    const uint32_t c = b % nCU, s = w & 3u;
-    kind = 0;
-    if (c < hc) {
-        if (r == 0) { kind = 1; return c * 4u + s; }
-        if (r >= keep) { kind = 2; return 0u; }
-    }
-    if (r == 0) return 4u * hc + s * rest + (c - hc);
-    if (r < keep) {
-        const uint32_t idx = s * nCU + c;
-        return r * per + ((r & 1u) ? per - 1u - idx : idx);
-    }
-    const uint32_t idx = s * rest + (c - hc), q = r - keep;
-    return keep * per + q * per2 + ((q & 1u) ? per2 - 1u - idx : idx);
-}
-
-// A waiting wave polls its SIMD's flag (an L2 read every ~3 us; asleep in between).  Bounded: after
-// ~7 s of shader clock it goes on regardless (only the schedule would change), so every wave of the
-// grid reaches its exit.
-constexpr uint64_t kQuietWaitMax = 1ull << 34;
-PT_DEV void quiet_wait(uint32_t* flag)
-{
-    const uint64_t t0 = __builtin_amdgcn_s_memtime();
-    for (;;) {
-        const uint32_t v = __hip_atomic_load(flag, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        if (__builtin_amdgcn_readfirstlane(v) != 0u) break;
-        if (__builtin_amdgcn_s_memtime() - t0 > kQuietWaitMax) break;
-        __builtin_amdgcn_s_sleep(64);
-    }
-}
-
-// The quiet flag of the calling wave's SIMD (its CU and SIMD as quiet_slot counts them).
-template <int WPB>
-PT_DEV uint32_t* quiet_flag(const TraceParams& P)
-{
-    return P.quietFlag + (blockIdx.x % P.spreadCU) * 4u + (__builtin_amdgcn_readfirstlane(threadIdx.x >> 6) & 3u);
-}
-
 template <bool STATS, int SL, int WPB, int WW, int MINW, bool PERSIST = false, int MODE = 0>
 __global__ void __launch_bounds__(WPB * 64, MINW) trace_kernel(TraceParams P)
 {
@@ -350,56 +299,22 @@ __global__ void __launch_bounds__(WPB * 64, MINW) trace_kernel(TraceParams P)
     stage_scene_impl<SL, WPB, WW>(P);
     Counters cnt = {};
     const bool spread = PERSIST && P.spreadCU != 0;
-    const bool quiet = spread && P.quietCU != 0;
-    const uint32_t keep = 1u + P.quietCap;
-    // quiet: the positions dealt are [0, base); rounds = resident waves per SIMD (host: CU-count multiple)
-    const uint32_t base = quiet ? keep * 4u * P.spreadCU +
-                                  (gridDim.x * (uint32_t)WPB / (4u * P.spreadCU) - keep) * 4u * (P.spreadCU - P.quietCU)
-                        : spread ? gridDim.x * (uint32_t)WPB : 0u;
-    uint32_t kind = 0;
+    const uint32_t base = spread ? gridDim.x * (uint32_t)WPB : 0u;
     uint32_t slot = !PERSIST ? __builtin_amdgcn_readfirstlane(blockIdx.x * (uint32_t)WPB + wave)
-                  : quiet    ? quiet_slot<WPB>(blockIdx.x, __builtin_amdgcn_readfirstlane(wave), P.spreadCU, P.quietCU, keep, kind)
                   : spread   ? spread_slot<WPB>(blockIdx.x, __builtin_amdgcn_readfirstlane(wave), P.spreadCU)
                              : wave_fetch(P.tileCursor, 1u);
-    // two-ended queue (backRound != 0): the waves of the later rounds -- the youngest, which lose
-    // equal-priority issue arbitration to the older waves of their SIMD -- take the cheapest positions
-    // from the back of the order, the older waves the expensive ones from the front.  Every fetch
-    // first claims one of the numSlots - base positions (word 0), then its end's next one (words 2 /
-    // 3), so the two ends never overlap.
-    const bool twoEnded = spread && P.backRound != 0;
-    const bool back = twoEnded &&
-                      (blockIdx.x / P.spreadCU) * (uint32_t)(WPB / 4) + (__builtin_amdgcn_readfirstlane(wave) >> 2) >= P.backRound;
-    auto next = [&]() -> uint32_t {
-        if (twoEnded) {
-            if (base + wave_fetch(P.tileCursor, 1u) >= P.numSlots) return P.numSlots;
-            return back ? P.numSlots - 1u - wave_fetch(P.tileCursor + 2, 1u) : base + wave_fetch(P.tileCursor + 3, 1u);
-        }
-        return base + wave_fetch(P.tileCursor, 1u);
-    };
-    if (quiet && kind == 2) {
-        quiet_wait(quiet_flag<WPB>(P));
-        slot = next();
-    }
     for (;;) {
     if (slot >= P.numSlots) break;               // also the grid's spare slots past the last item
-    // a head's position (< 4 x quietCU) is dealt to that head only: no other state marks it
-    const bool head = quiet && slot < 4u * P.quietCU;
     run_item<STATS, SL, WPB, WW, MINW, PERSIST, MODE>(P, slot, cnt);
-    if (head && lane == 0)                       // the head tile is done: its SIMD's waiting waves go on
-        __hip_atomic_store(quiet_flag<WPB>(P), 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     if (!PERSIST) break;
-    slot = next();
+    slot = base + wave_fetch(P.tileCursor, 1u);
     }
-    if (quiet && slot < 4u * P.quietCU && lane == 0)   // a head position past the last item
-        __hip_atomic_store(quiet_flag<WPB>(P), 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     if (PERSIST) {
-        // the last wave to leave rewinds the cursor (and clears the quiet flags) for the next launch
-        // (every wave has made its final fetch before it counts itself out), so no memset precedes
-        // the launch
-        if (wave_fetch(P.tileCursor + 1, 1u) == gridDim.x * (uint32_t)WPB - 1) {
-            if (quiet)
-                for (uint32_t i = lane; i < 4u * P.quietCU; i += 64u) P.quietFlag[i] = 0u;
-            if (lane < kCursorWords) P.tileCursor[lane] = 0;
+        // the last wave to leave rewinds the cursor for the next launch (every wave has made its
+        // final fetch before it counts itself out), so no memset precedes the launch
+        if (wave_fetch(P.tileCursor + 1, 1u) == gridDim.x * (uint32_t)WPB - 1 && lane == 0) {
+            P.tileCursor[0] = 0;
+            P.tileCursor[1] = 0;
         }
     }
     flush_counters<STATS>(P, cnt);
@@ -525,10 +440,6 @@ struct pt_context {
     uint32_t* unitMajor = nullptr;    // row-major order of strip units (packed first tiles), for unitK
     uint32_t unitK = 0, unitTiles = 0;
     uint32_t occupancy = 0;       // tuning knob: workgroups per CU of persistent grids (0 = all that fit)
-    uint32_t quietCUs = 0;        // quiet head CUs (pt_set_quiet_heads; 0 = off) and the waves beside each head
-    uint32_t quietCap = 0;
-    uint32_t lastQuiet = 0;       // quiet head CUs the last launch ran with
-    uint32_t backRound = 0;       // pt_set_two_ended_queue: first round of waves taking from the back (0 = off)
     uint32_t prioLevels = kPrioLevels;    // pt_set_issue_priority_levels: the level of each position band
     int prioMode = 0;             // issue priority: 0 = automatic, 1 = off, 2 = explicit bounds prioBounds
     uint32_t prioBounds[3] = {0, 0, 0};
@@ -588,8 +499,6 @@ static int fail(pt_context* ctx, int code, const char* msg)
 }
 
 // Kernel variants (workgroup size, scene staged in LDS or read through the caches).
-// quiet head CUs the last persistent launch of this host thread applied (pt_last_quiet_heads)
-static thread_local uint32_t tl_quietApplied = 0;
 
 template <bool STATS, int SL, int WPB, int WW, int MINW, bool PERSIST = false, int MODE = 0>
 static hipError_t launch_one(const TraceParams& P, hipStream_t stream)
@@ -646,11 +555,18 @@ static hipError_t launch_one(const TraceParams& P, hipStream_t stream)
         if (cap <= 0) return hipErrorInvalidValue;
         TraceParams Q = P;                             // first slots dealt per SIMD (spread_slot)
         Q.spreadCU = (cus > 0 && WPB % 4 == 0 && cap % cus == 0) ? (uint32_t)cus : 0u;
-        // quiet head CUs need a spread grid with more waves per SIMD than the head keeps beside it
-        const uint32_t rounds = Q.spreadCU ? (uint32_t)cap * WPB / (4u * (uint32_t)cus) : 0u;
-        if (!Q.spreadCU || !P.quietFlag || 1u + P.quietCap >= rounds || 4u * (uint32_t)cus > kQuietWords) Q.quietCU = 0;
-        Q.quietCU = std::min<uint32_t>(Q.quietCU, (uint32_t)cus);
-        tl_quietApplied = Q.quietCU;
+        if (P.prioDealt) {
+            // Every position dealt at the start runs in the first priority band.  Waves of equal
+            // priority issue oldest first (the resident grid's dispatch order: tools/tile_trace.py shows
+            // the dealing rounds' tiles at 160 / 175 / 235 / 275 ms median and the last round's, at level
+            // 2 below the others, at 373 ms -- the launch's end on the C4 N = 8 share); in one band the
+            // order of the rounds follows the cost order.  C4 N = 8 share 464-481 -> 446-456 ms
+            // (tools/prio_probe.py, profiles/r06_schedule_trace.json).
+            const uint32_t dealt = std::min<uint32_t>(P.numSlots, (uint32_t)cap * WPB);
+            Q.prio[0] = std::max(Q.prio[0], dealt);
+            Q.prio[1] = std::max(Q.prio[1], Q.prio[0]);
+            Q.prio[2] = std::max(Q.prio[2], Q.prio[1]);
+        }
         trace_kernel<STATS, SL, WPB, WW, MINW, PERSIST, MODE><<<(unsigned)cap, WPB * 64, lds, stream>>>(Q);
         return hipGetLastError();
     }
@@ -1548,14 +1464,13 @@ static int render_impl(pt_context* ctx, const pt_camera* cam, uint32_t spp, uint
     P.tileCost = sorted ? ctx->tileCost : nullptr;
     P.scatterWaves = ctx->schedule == 2 ? (uint32_t)(((size_t)ctx->rows * ctx->width + 63) / 64) : 0u;
     if (P.scatterWaves) P.order = nullptr;          // scattered mapping: slot = wave index
-    if (!ctx->tileCursor) {                         // {cursor, waves out, back, front}, then the quiet flags
-        PT_HIP_CHECK(ctx, hipMalloc(&ctx->tileCursor, (kCursorWords + kQuietWords) * sizeof(uint32_t)));
-        PT_HIP_CHECK(ctx, hipMemset(ctx->tileCursor, 0, (kCursorWords + kQuietWords) * sizeof(uint32_t)));
+    if (!ctx->tileCursor) {
+        PT_HIP_CHECK(ctx, hipMalloc(&ctx->tileCursor, 2 * sizeof(uint32_t)));
+        PT_HIP_CHECK(ctx, hipMemset(ctx->tileCursor, 0, 2 * sizeof(uint32_t)));
     }
     P.tileCursor = ctx->tileCursor;
     P.numSlots = units;
     P.occCap = ctx->occupancy;
-    P.backRound = ctx->backRound;
     P.prioVal = ctx->prioLevels;
     // Issue priority follows the order position, so it is meaningful only on a current cost order.
     // A launch whose tile costs will rebuild the order (stale order, or this launch measures >= 4x
@@ -1565,6 +1480,7 @@ static int render_impl(pt_context* ctx, const pt_camera* cam, uint32_t spp, uint
     const bool rebuilds = ctx->schedule == 0 &&
                           (ctx->orderStale || !ctx->orderValid || (uint64_t)spp * chunks >= 4 * ctx->orderSamples);
     if (!rebuilds || ctx->prioMode == 2) issue_priority(ctx, units, P.prio);   // explicit bounds: always
+    P.prioDealt = ctx->prioMode == 0 && P.prio[0] != 0;
     if (ctx->traceTiles && P.tileCost) {
         if (ctx->tileTrace && ctx->traceCap < tiles) {
             (void)hipFree(ctx->tileTrace);
@@ -1656,6 +1572,7 @@ static int render_impl(pt_context* ctx, const pt_camera* cam, uint32_t spp, uint
         Q.chunks = 1;
         Q.order = firstOrder;
         for (int i = 0; i < 3; ++i) Q.prio[i] = 0;        // row-major positions: no priority grading
+        Q.prioDealt = 0;
         PT_HIP_CHECK(ctx, launch_variant<false>(variant, Q, ctx->stream));
         const int rs = sort_order(ctx, tiles, spp, K);
         if (rs != PT_OK) return rs;
@@ -1664,6 +1581,7 @@ static int render_impl(pt_context* ctx, const pt_camera* cam, uint32_t spp, uint
         P.ignoreFirst = 0;                               // the first call is done
         if (ctx->coldPriority && ctx->prioMode == 0) {
             issue_priority(ctx, units, P.prio);
+            P.prioDealt = 1;
             biasedOrder = true;
         }
     } else if (cold) {
@@ -1677,6 +1595,7 @@ static int render_impl(pt_context* ctx, const pt_camera* cam, uint32_t spp, uint
         Q.discard = 1;
         Q.order = firstOrder;
         for (int i = 0; i < 3; ++i) Q.prio[i] = 0;        // row-major positions: no priority grading
+        Q.prioDealt = 0;
         Q.pairsOut = guesses && ssg_reserve(ctx, tiles, 0, 0, 0) ? ctx->pairs : nullptr;
         if (Q.pairsOut) ctx->pairsValid = true;
         PT_HIP_CHECK(ctx, Q.pairsOut ? launch_grouped<2>(variant, Q, ctx->stream)
@@ -1686,19 +1605,13 @@ static int render_impl(pt_context* ctx, const pt_camera* cam, uint32_t spp, uint
         P.order = ctx->order;
         if (ctx->coldPriority && ctx->prioMode == 0) {
             issue_priority(ctx, units, P.prio);
+            P.prioDealt = 1;
             biasedOrder = true;
         }
     }
-    // quiet head CUs (quiet_slot): plain launches on a current cost order only (the head positions must
-    // be the heaviest tiles, and costs measured with quiet heads would rank them lower)
-    if (!G && K == 1 && !ahead && !cold && !rebuilds && ctx->quietCUs) {
-        P.quietCU = ctx->quietCUs;
-        P.quietCap = ctx->quietCap;
-        P.quietFlag = ctx->tileCursor + kCursorWords;
-    }
-    tl_quietApplied = 0;
     if (G && P.tileCost) PT_HIP_CHECK(ctx, hipMemsetAsync(P.tileCost, 0, (size_t)tiles * sizeof(uint32_t), ctx->stream));
     if (G) {
+        P.prioDealt = 0;           // (grouped positions are (tile, group) items: measured slower with it)
         const int rc = run_groups(ctx, variant, P, G, tiles, ssgCap, ctx->stream);
         if (rc != PT_OK) return rc;
         ctx->lastGroups = G;
@@ -1707,7 +1620,6 @@ static int render_impl(pt_context* ctx, const pt_camera* cam, uint32_t spp, uint
                                 : ahead ? launch_ahead(variant, P, ctx->stream)
                                 : (K > 1 ? launch_strip(variant, P, ctx->stream) : launch_variant<false>(variant, P, ctx->stream)));
     }
-    ctx->lastQuiet = P.quietCU ? tl_quietApplied : 0u;
     if (aheadMake) {
         ctx->aheadValid = true;
         ctx->aheadCam = *cam;
@@ -1856,26 +1768,6 @@ PT_API int pt_set_issue_priority(pt_context* ctx, int mode, uint32_t level3, uin
     ctx->prioBounds[1] = level2;
     ctx->prioBounds[2] = level1;
     return PT_OK;
-}
-
-PT_API int pt_set_quiet_heads(pt_context* ctx, uint32_t cus, uint32_t beside)
-{
-    if (!ctx || cus > kQuietWords / 4 || beside > 15) return PT_ERR_ARG;
-    ctx->quietCUs = cus;
-    ctx->quietCap = beside;
-    return PT_OK;
-}
-
-PT_API int pt_set_two_ended_queue(pt_context* ctx, uint32_t back_round)
-{
-    if (!ctx || back_round > 64) return PT_ERR_ARG;
-    ctx->backRound = back_round;
-    return PT_OK;
-}
-
-PT_API int pt_last_quiet_heads(const pt_context* ctx)
-{
-    return ctx ? (int)ctx->lastQuiet : PT_ERR_ARG;
 }
 
 PT_API int pt_set_issue_priority_levels(pt_context* ctx, uint32_t l0, uint32_t l1, uint32_t l2, uint32_t l3)

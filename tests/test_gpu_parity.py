@@ -169,12 +169,11 @@ def test_schedule_knobs_do_not_change_results(gpu_available, scenes):
         assert np.array_equal(pt.rng_state(), want_rng), (prio, occ)
 
 
-def test_quiet_heads_do_not_change_results(gpu_available, scenes):
-    # quiet head CUs (pt_set_quiet_heads): heads on their own SIMDs, waves beside them capped, the
-    # rest asleep until their head is done -- every position runs once, the bits stay the same.  The
-    # five-wave build (automatic at 2.3 tiles per six-wave slot) and the forced six- and four-wave
-    # builds; a grid capped at 2 waves per SIMD with 1 beside the head leaves no wave to wait and runs
-    # without quiet CUs.
+def test_priority_levels_do_not_change_results(gpu_available, scenes):
+    # issue priority levels per cost-order band (pt_set_issue_priority_levels), with the automatic
+    # bounds (the dealt positions raised into the first band) and explicit ones, on the five-wave
+    # build (automatic at 2.3 tiles per six-wave slot) and the forced six- and four-wave builds: only
+    # which wave issues first changes
     W, H = 1280, 720
     pt = pa.Pathtracer(W, H)
     cam = pt.load_scene(scenes / "generated_scene.scene.json")
@@ -184,35 +183,20 @@ def test_quiet_heads_do_not_change_results(gpu_available, scenes):
     pt.render(cam, 4, True, chunks=3)
     want = pt.accum().view(np.uint32).copy()
     want_rng = pt.rng_state()
-    assert pt.last_quiet_heads == 0
-    for variant, occ, cus, beside, applied in [(0, 0, 64, 2, 64), (0, 0, 64, 0, 64), (0, 0, 256, 3, 256),
-                                               (0, 0, 1000, 1, 256), (0, 0, 8, 1, 8), (60, 0, 64, 2, 64),
-                                               (46, 0, 32, 1, 32), (0, 3, 32, 1, 32), (0, 2, 32, 1, 0)]:
+    for variant, bounds, levels in [(0, None, (0, 1, 2, 3)), (0, (5120, 5120, 12000), (3, 3, 1, 0)),
+                                    (60, None, (3, 3, 1, 0)), (46, (100, 7000, 7000), (2, 3, 3, 0))]:
         pt.set_kernel_variant(variant)
-        pt.set_occupancy(occ)
-        pt.set_quiet_heads(cus, beside)
-        for _ in range(2):                            # the flags are cleared for the next launch
-            pt.set_rng_state(st)
-            pt.render(cam, 4, True, chunks=3)
-            assert pt.last_quiet_heads == applied, (variant, occ, cus, beside)
-            assert np.array_equal(pt.accum().view(np.uint32), want), (variant, occ, cus, beside)
-            assert np.array_equal(pt.rng_state(), want_rng), (variant, occ, cus, beside)
-    pt.set_quiet_heads(0, 0)
-    pt.set_occupancy(0)
-    # two-ended queue (youngest rounds from the back of the order) and reordered priority levels
-    for variant, back, levels in [(0, 3, (3, 2, 1, 0)), (0, 1, (0, 1, 2, 3)), (60, 4, (3, 3, 1, 0)), (46, 2, (2, 3, 3, 0))]:
-        pt.set_kernel_variant(variant)
-        pt.set_two_ended_queue(back)
+        if bounds:
+            pt.set_issue_priority(2, *bounds)
+        else:
+            pt.set_issue_priority(0)
         pt.set_issue_priority_levels(*levels)
-        pt.set_quiet_heads(32 if back == 3 else 0, 1)
-        for _ in range(2):
-            pt.set_rng_state(st)
-            pt.render(cam, 4, True, chunks=3)
-            assert np.array_equal(pt.accum().view(np.uint32), want), (variant, back, levels)
-            assert np.array_equal(pt.rng_state(), want_rng), (variant, back, levels)
-    pt.set_two_ended_queue(0)
+        pt.set_rng_state(st)
+        pt.render(cam, 4, True, chunks=3)
+        assert np.array_equal(pt.accum().view(np.uint32), want), (variant, bounds, levels)
+        assert np.array_equal(pt.rng_state(), want_rng), (variant, bounds, levels)
+    pt.set_issue_priority(0)
     pt.set_issue_priority_levels(3, 2, 1, 0)
-    pt.set_quiet_heads(0, 0)
     pt.set_kernel_variant(0)
 
 

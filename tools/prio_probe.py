@@ -2,10 +2,9 @@
 throughout): launch time, and with --trace the last tile ends per position band (per-CU clocks).
     python tools/prio_probe.py [--n 8 --rank 2 --width 3840 --height 2160 --spp 4096]
                                [--settings a,5120/8160/12240@3210] [--rounds 3] [--trace]
-A setting is "a" (automatic) or B0/B1/B2@L0L1L2L3[+CUS:BESIDE][~R]: positions < B0 at level L0, < B1
-at L1, < B2 at L2, the rest at L3 (pt_set_issue_priority mode 2 + pt_set_issue_priority_levels), with
-optional quiet head CUs (pt_set_quiet_heads) and a two-ended queue from dealing round R
-(pt_set_two_ended_queue); "a~R" = automatic priority with a two-ended queue.  Bounds may be written as fractions of the tiles
+A setting is "a" (automatic) or B0/B1/B2@L0L1L2L3: positions < B0 at level L0, < B1 at L1, < B2 at L2,
+the rest at L3 (pt_set_issue_priority mode 2 + pt_set_issue_priority_levels).  (Quiet head CUs and a
+two-ended queue were probed with this tool at commit 3c9fd51.)  Bounds may be written as fractions of the tiles
 (e.g. 0.25).
 """
 import argparse
@@ -44,20 +43,16 @@ pos_of[np.argsort(-ref.astype(np.int64), kind="stable")] = np.arange(n)
 
 
 def apply(tok):
-    tok, _, r = tok.partition("~")
-    pt.set_two_ended_queue(int(r or 0))
-    m = re.fullmatch(r"([\d.]+)/([\d.]+)/([\d.]+)@([0-3])([0-3])([0-3])([0-3])(?:\+(\d+):(\d+))?", tok)
+    m = re.fullmatch(r"([\d.]+)/([\d.]+)/([\d.]+)@([0-3])([0-3])([0-3])([0-3])", tok)
     if tok == "a":
         pt.set_issue_priority(0)
         pt.set_issue_priority_levels(3, 2, 1, 0)
-        pt.set_quiet_heads(0, 0)
         return
     if not m:
         raise SystemExit(f"bad setting {tok}")
     b = [int(float(x) * n) if "." in x else int(x) for x in m.groups()[:3]]
     pt.set_issue_priority(2, *b)
     pt.set_issue_priority_levels(*(int(x) for x in m.groups()[3:7]))
-    pt.set_quiet_heads(int(m.group(8) or 0), int(m.group(9) or 0))
 
 
 def ends(tr, dur):
@@ -99,8 +94,7 @@ for r in range(a.rounds):
             last = np.argsort(-en)[:10]
             e["last"] = [[int(pos_of[i]), round(float(st[i]), 1), round(float(dur[i]), 1), int(hw[i] & 15)] for i in last]
             SAVE[s] = (st, dur, hw)
-        print(json.dumps({"round": r, "setting": s, "ms": round(ms, 2), "variant": pt.last_variant,
-                          "quiet": pt.last_quiet_heads}), flush=True)
+        print(json.dumps({"round": r, "setting": s, "ms": round(ms, 2), "variant": pt.last_variant}), flush=True)
 apply("a")
 if a.out and SAVE:
     arrs = {"pos_of": pos_of}
