@@ -204,8 +204,8 @@ PT_API int pt_read_tile_costs(pt_context *ctx, uint32_t *dst, uint32_t count);
  * (resumable variants).  Divided by the tile's cycles (pt_read_tile_costs) it is the tile's
  * idle-lane fraction. */
 PT_API int pt_read_tile_idle(pt_context *ctx, uint32_t *dst, uint32_t count);
-/* Diagnostics: schedule trace.  With enabled != 0 every launch that records tile costs also records
- * per tile (row-major) two words: the shader-clock cycle (low 32 bits) at which its wave started it,
+/* Diagnostics: schedule trace.  With enabled != 0 every instrumented launch (pt_render_instrumented;
+ * the plain kernel carries no trace code) also records per tile (row-major) two words: the shader-clock cycle (low 32 bits) at which its wave started it,
  * and the wave's hardware ids (XCC_ID << 16 | HW_ID bits 0-15: wave, SIMD, pipe, CU, SH, SE).
  * pt_read_tile_trace reads the last such launch's 2 x tiles words.  Results are unchanged. */
 PT_API int pt_set_tile_trace(pt_context *ctx, int enabled);
@@ -242,9 +242,6 @@ PT_API int pt_set_occupancy(pt_context *ctx, uint32_t workgroups_per_cu);
  * 2 = explicit -- positions < level3 run at wave priority 3, < level2 at 2, < level1 at 1, the
  * rest at 0 (level3 <= level2 <= level1).  Results are identical. */
 PT_API int pt_set_issue_priority(pt_context *ctx, int mode, uint32_t level3, uint32_t level2, uint32_t level1);
-/* The wave priority (0..3) of each of the four position bands above, head band first (default 3, 2,
- * 1, 0).  Results are identical. */
-PT_API int pt_set_issue_priority_levels(pt_context *ctx, uint32_t l0, uint32_t l1, uint32_t l2, uint32_t l3);
 
 /* Speculative sample groups.  A pixel's samples are one serial XORWOW stream
  * (trace.cu:183-193), so a launch with fewer 8x8 tiles than about four per wave slot of the chip

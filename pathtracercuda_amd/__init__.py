@@ -305,12 +305,6 @@ class Pathtracer:
         for c in self._contexts():
             N.check_ctx(N.hip().pt_set_occupancy(c, int(workgroups_per_cu)), c)
 
-    def set_issue_priority_levels(self, l0: int = 3, l1: int = 2, l2: int = 1, l3: int = 0) -> None:
-        """Wave priority of each of the four cost-order position bands (pt_set_issue_priority_levels);
-        the default 3, 2, 1, 0 ranks the head first.  Results are identical."""
-        for c in self._contexts():
-            N.check_ctx(N.hip().pt_set_issue_priority_levels(c, int(l0), int(l1), int(l2), int(l3)), c)
-
     def set_issue_priority(self, mode: int, level3: int = 0, level2: int = 0, level1: int = 0) -> None:
         """Issue priority by cost-order position (pt_set_issue_priority): mode 0 automatic, 1 off,
         2 explicit (positions < level3 at priority 3, < level2 at 2, < level1 at 1).  Results are
@@ -418,7 +412,8 @@ class Pathtracer:
         return out.reshape(ty, tx)
 
     def set_tile_trace(self, enabled: bool) -> None:
-        """Record per tile the start cycle and hardware ids of the wave that ran it (diagnostics)."""
+        """Instrumented launches also record per tile the start cycle and hardware ids of the wave
+        that ran it (diagnostics)."""
         for c in self._contexts():
             N.check_ctx(N.hip().pt_set_tile_trace(c, int(bool(enabled))), c)
 

@@ -84,7 +84,6 @@ _HIP_SYMBOLS = {
     "pt_set_kernel_variant": (C.c_int, [C.c_void_p, C.c_int]),
     "pt_set_occupancy": (C.c_int, [C.c_void_p, C.c_uint32]),
     "pt_set_tile_trace": (C.c_int, [C.c_void_p, C.c_int]),
-    "pt_set_issue_priority_levels": (C.c_int, [C.c_void_p, C.c_uint32, C.c_uint32, C.c_uint32, C.c_uint32]),
     "pt_read_tile_trace": (C.c_int, [C.c_void_p, P(C.c_uint32), C.c_uint32]),
     "pt_set_issue_priority": (C.c_int, [C.c_void_p, C.c_int, C.c_uint32, C.c_uint32, C.c_uint32]),
     "pt_set_schedule": (C.c_int, [C.c_void_p, C.c_int]),

@@ -43,7 +43,7 @@ struct TraceParams {
     uint32_t* tileCursor;       // persistent variants: {next dispatch slot, waves finished}, rewound by the last wave
     uint32_t numSlots;          // dispatch slots = 8x8 tiles
     uint32_t* tileCost;         // per-tile shader-clock cycles of this launch (null: not recorded)
-    uint32_t* tileTrace;        // schedule trace (pt_set_tile_trace): per tile {start cycles, XCC << 16 | HW_ID}
+    uint32_t* tileTrace;        // instrumented launches, pt_set_tile_trace: per tile {start cycles, XCC << 16 | HW_ID}
     uint32_t* tileIdle;         // instrumented launches: per tile, the lanes' mean cycles between finishing
                                 // their pixel and the tile's end (zeroed before the launch)
     uint32_t discard;           // != 0: cost pre-pass -- pixel state (RNG, accum) is read, never written
@@ -70,8 +70,7 @@ struct TraceParams {
     uint32_t* fold;             // [kFoldWords][rows*width] fold state (ssg_fold_kernel); AUX resume input
     DevCamera cam;
     uint32_t occCap;            // host only: persistent grids hold at most this many workgroups per CU (0 = all)
-    uint32_t prio[3];           // issue priority by order position: bands < prio[0], < prio[1], < prio[2], the rest
-    uint32_t prioVal;           // the bands' levels, 2 bits each from bit 0 (kPrioLevels: 3, 2, 1, 0)
+    uint32_t prio[3];           // issue priority by order position: < prio[0] -> 3, < prio[1] -> 2, < prio[2] -> 1
     uint32_t strip;             // MODE 3: tiles per dispatch unit (a row strip of `strip` tiles; see trace_kernel)
     // MODE 4 (run-ahead across render() calls, see trace_kernel): per-pixel stash of the NEXT call's
     // first samples, kAheadWords planes of rows x width u32 (ahead_store).
@@ -82,7 +81,6 @@ struct TraceParams {
     uint32_t prioDealt;         // host only: persistent grids raise the first band to every position dealt
                                 // at the start (launch_one; automatic priority)
 };
-constexpr uint32_t kPrioLevels = 3u | 2u << 2 | 1u << 4 | 0u << 6;    // default band levels 3, 2, 1, 0
 
 // Speculative sample groups: window of a group's start offset in which an earlier group's parse can
 // join it (draw pairs; 16 x 64-bit words per lane), and the fold state kept per pixel between rounds.

@@ -135,12 +135,9 @@ PT_DEV void run_item(const TraceParams& P, uint32_t slot, Counters& cnt)
     // end the launch.  Waves on the head of the order take issue slots first (s_setprio), the rest
     // fill the gaps.  pos is wave-uniform (an SGPR), so only one s_setprio executes.  Scheduling
     // only: results are identical.
-    // The level of each band is a 2-bit field of prioVal (default 3, 2, 1, 0).
-    const uint32_t band = pos < P.prio[0] ? 0u : pos < P.prio[1] ? 1u : pos < P.prio[2] ? 2u : 3u;
-    const uint32_t level = (P.prioVal >> (2u * band)) & 3u;
-    if (level == 3u) __builtin_amdgcn_s_setprio(3);
-    else if (level == 2u) __builtin_amdgcn_s_setprio(2);
-    else if (level == 1u) __builtin_amdgcn_s_setprio(1);
+    if (pos < P.prio[0]) __builtin_amdgcn_s_setprio(3);
+    else if (pos < P.prio[1]) __builtin_amdgcn_s_setprio(2);
+    else if (pos < P.prio[2]) __builtin_amdgcn_s_setprio(1);
     else __builtin_amdgcn_s_setprio(0);
     PixelCtx pc = pixel_of(P, tile, lane);
     const uint64_t tWave = __builtin_amdgcn_s_memtime();
@@ -254,7 +251,7 @@ PT_DEV void run_item(const TraceParams& P, uint32_t slot, Counters& cnt)
         // SSG: zeroed before the launch (idle items add ~0)
         if (SSG) atomicAdd(&P.tileCost[lin], cyc / P.ssgG);
         else P.tileCost[lin] = cyc;
-        if (P.tileTrace) {                       // schedule trace (pt_set_tile_trace): start, hardware ids
+        if (STATS && P.tileTrace) {              // schedule trace (pt_set_tile_trace): start, hardware ids
             P.tileTrace[2 * lin] = (uint32_t)tWave;
             P.tileTrace[2 * lin + 1] = (__builtin_amdgcn_s_getreg((31 << 11) | (0 << 6) | 20) << 16) |
                                        (__builtin_amdgcn_s_getreg((31 << 11) | (0 << 6) | 4) & 0xffffu);
@@ -440,7 +437,6 @@ struct pt_context {
     uint32_t* unitMajor = nullptr;    // row-major order of strip units (packed first tiles), for unitK
     uint32_t unitK = 0, unitTiles = 0;
     uint32_t occupancy = 0;       // tuning knob: workgroups per CU of persistent grids (0 = all that fit)
-    uint32_t prioLevels = kPrioLevels;    // pt_set_issue_priority_levels: the level of each position band
     int prioMode = 0;             // issue priority: 0 = automatic, 1 = off, 2 = explicit bounds prioBounds
     uint32_t prioBounds[3] = {0, 0, 0};
     // speculative sample groups
@@ -1471,7 +1467,6 @@ static int render_impl(pt_context* ctx, const pt_camera* cam, uint32_t spp, uint
     P.tileCursor = ctx->tileCursor;
     P.numSlots = units;
     P.occCap = ctx->occupancy;
-    P.prioVal = ctx->prioLevels;
     // Issue priority follows the order position, so it is meaningful only on a current cost order.
     // A launch whose tile costs will rebuild the order (stale order, or this launch measures >= 4x
     // the samples the order came from; see the rebuild below) runs without it: graded priority
@@ -1767,13 +1762,6 @@ PT_API int pt_set_issue_priority(pt_context* ctx, int mode, uint32_t level3, uin
     ctx->prioBounds[0] = level3;
     ctx->prioBounds[1] = level2;
     ctx->prioBounds[2] = level1;
-    return PT_OK;
-}
-
-PT_API int pt_set_issue_priority_levels(pt_context* ctx, uint32_t l0, uint32_t l1, uint32_t l2, uint32_t l3)
-{
-    if (!ctx || l0 > 3 || l1 > 3 || l2 > 3 || l3 > 3) return PT_ERR_ARG;
-    ctx->prioLevels = l0 | l1 << 2 | l2 << 4 | l3 << 6;
     return PT_OK;
 }
 

@@ -169,11 +169,11 @@ def test_schedule_knobs_do_not_change_results(gpu_available, scenes):
         assert np.array_equal(pt.rng_state(), want_rng), (prio, occ)
 
 
-def test_priority_levels_do_not_change_results(gpu_available, scenes):
-    # issue priority levels per cost-order band (pt_set_issue_priority_levels), with the automatic
-    # bounds (the dealt positions raised into the first band) and explicit ones, on the five-wave
-    # build (automatic at 2.3 tiles per six-wave slot) and the forced six- and four-wave builds: only
-    # which wave issues first changes
+def test_priority_bounds_and_trace_do_not_change_results(gpu_available, scenes):
+    # issue-priority bounds, automatic (the dealt positions raised into the first band) and explicit,
+    # on the five-wave build (automatic at 2.3 tiles per six-wave slot) and the forced six- and
+    # four-wave builds, plain and instrumented with the schedule trace: only which wave issues first
+    # changes.  The trace holds one start and one hardware id per tile.
     W, H = 1280, 720
     pt = pa.Pathtracer(W, H)
     cam = pt.load_scene(scenes / "generated_scene.scene.json")
@@ -183,20 +183,26 @@ def test_priority_levels_do_not_change_results(gpu_available, scenes):
     pt.render(cam, 4, True, chunks=3)
     want = pt.accum().view(np.uint32).copy()
     want_rng = pt.rng_state()
-    for variant, bounds, levels in [(0, None, (0, 1, 2, 3)), (0, (5120, 5120, 12000), (3, 3, 1, 0)),
-                                    (60, None, (3, 3, 1, 0)), (46, (100, 7000, 7000), (2, 3, 3, 0))]:
+    pt.set_tile_trace(True)
+    for variant, bounds in [(0, None), (0, (5120, 5120, 12000)), (60, None), (46, (100, 7000, 7000))]:
         pt.set_kernel_variant(variant)
         if bounds:
             pt.set_issue_priority(2, *bounds)
         else:
             pt.set_issue_priority(0)
-        pt.set_issue_priority_levels(*levels)
-        pt.set_rng_state(st)
-        pt.render(cam, 4, True, chunks=3)
-        assert np.array_equal(pt.accum().view(np.uint32), want), (variant, bounds, levels)
-        assert np.array_equal(pt.rng_state(), want_rng), (variant, bounds, levels)
+        for instrumented in (False, True):
+            pt.set_rng_state(st)
+            if instrumented:
+                pt.render_instrumented(cam, 4, 3, True)
+                tr = pt.tile_trace().reshape(-1, 2)
+                cu = (tr[:, 1] >> 16) << 8 | ((tr[:, 1] & 0xffff) >> 8)
+                assert len(np.unique(cu)) > 200, "tiles ran on every CU"
+            else:
+                pt.render_raw(cam, 4, 3, True)
+            assert np.array_equal(pt.accum().view(np.uint32), want), (variant, bounds, instrumented)
+            assert np.array_equal(pt.rng_state(), want_rng), (variant, bounds, instrumented)
+    pt.set_tile_trace(False)
     pt.set_issue_priority(0)
-    pt.set_issue_priority_levels(3, 2, 1, 0)
     pt.set_kernel_variant(0)
 
 

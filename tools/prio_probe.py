@@ -2,9 +2,10 @@
 throughout): launch time, and with --trace the last tile ends per position band (per-CU clocks).
     python tools/prio_probe.py [--n 8 --rank 2 --width 3840 --height 2160 --spp 4096]
                                [--settings a,5120/8160/12240@3210] [--rounds 3] [--trace]
-A setting is "a" (automatic) or B0/B1/B2@L0L1L2L3: positions < B0 at level L0, < B1 at L1, < B2 at L2,
-the rest at L3 (pt_set_issue_priority mode 2 + pt_set_issue_priority_levels).  (Quiet head CUs and a
-two-ended queue were probed with this tool at commit 3c9fd51.)  Bounds may be written as fractions of the tiles
+A setting is "a" (automatic) or B0/B1/B2: positions < B0 at priority 3, < B1 at 2, < B2 at 1, the rest
+at 0 (pt_set_issue_priority mode 2).  (Other level orders per band, quiet head CUs and a two-ended
+queue were probed with this tool at commit 3c9fd51, profiles/r06_schedule_trace.json.)  --trace runs
+the instrumented build (the plain kernel carries no trace code): same schedule rules, ~15 % slower.  Bounds may be written as fractions of the tiles
 (e.g. 0.25).
 """
 import argparse
@@ -43,16 +44,14 @@ pos_of[np.argsort(-ref.astype(np.int64), kind="stable")] = np.arange(n)
 
 
 def apply(tok):
-    m = re.fullmatch(r"([\d.]+)/([\d.]+)/([\d.]+)@([0-3])([0-3])([0-3])([0-3])", tok)
+    m = re.fullmatch(r"([\d.]+)/([\d.]+)/([\d.]+)", tok)
     if tok == "a":
         pt.set_issue_priority(0)
-        pt.set_issue_priority_levels(3, 2, 1, 0)
         return
     if not m:
         raise SystemExit(f"bad setting {tok}")
     b = [int(float(x) * n) if "." in x else int(x) for x in m.groups()[:3]]
     pt.set_issue_priority(2, *b)
-    pt.set_issue_priority_levels(*(int(x) for x in m.groups()[3:7]))
 
 
 def ends(tr, dur):
@@ -79,7 +78,7 @@ pt.set_tile_trace(a.trace)
 for r in range(a.rounds):
     for s in settings:
         apply(s)
-        ms = pt.render_raw(cam, 8, chunks, True)
+        ms = pt.render_instrumented(cam, 8, chunks, True)["ms"] if a.trace else pt.render_raw(cam, 8, chunks, True)
         e = res[s]
         e["ms"].append(round(ms, 2))
         if a.trace:
