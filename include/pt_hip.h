@@ -205,8 +205,9 @@ PT_API int pt_read_tile_costs(pt_context *ctx, uint32_t *dst, uint32_t count);
  * idle-lane fraction. */
 PT_API int pt_read_tile_idle(pt_context *ctx, uint32_t *dst, uint32_t count);
 /* Diagnostics: schedule trace.  With enabled != 0 every instrumented launch (pt_render_instrumented;
- * the plain kernel carries no trace code) also records per tile (row-major) two words: the shader-clock cycle (low 32 bits) at which its wave started it,
- * and the wave's hardware ids (XCC_ID << 16 | HW_ID bits 0-15: wave, SIMD, pipe, CU, SH, SE).
+ * the plain kernel carries no trace code) also records per tile (row-major) two words: the
+ * shader-clock cycle (low 32 bits; the counter is per CU) at which its wave started it, and the
+ * wave's hardware ids (XCC_ID << 16 | HW_ID bits 0-15: wave, SIMD, pipe, CU, SH, SE).
  * pt_read_tile_trace reads the last such launch's 2 x tiles words.  Results are unchanged. */
 PT_API int pt_set_tile_trace(pt_context *ctx, int enabled);
 PT_API int pt_read_tile_trace(pt_context *ctx, uint32_t *dst, uint32_t count);
@@ -237,10 +238,10 @@ PT_API int pt_set_schedule(pt_context *ctx, int mode);
  * fit, the default).  Results are identical. */
 PT_API int pt_set_occupancy(pt_context *ctx, uint32_t workgroups_per_cu);
 
-
-/* Issue priority by position in the cost order (s_setprio): mode 0 = automatic (default), 1 = off,
- * 2 = explicit -- positions < level3 run at wave priority 3, < level2 at 2, < level1 at 1, the
- * rest at 0 (level3 <= level2 <= level1).  Results are identical. */
+/* Issue priority by position in the cost order (s_setprio): mode 0 = automatic (default: graded by
+ * quarter of the order, the first band raised to every position a persistent plain launch deals at
+ * its start), 1 = off, 2 = explicit -- positions < level3 run at wave priority 3, < level2 at 2,
+ * < level1 at 1, the rest at 0 (level3 <= level2 <= level1).  Results are identical. */
 PT_API int pt_set_issue_priority(pt_context *ctx, int mode, uint32_t level3, uint32_t level2, uint32_t level1);
 
 /* Speculative sample groups.  A pixel's samples are one serial XORWOW stream

@@ -495,7 +495,6 @@ static int fail(pt_context* ctx, int code, const char* msg)
 }
 
 // Kernel variants (workgroup size, scene staged in LDS or read through the caches).
-
 template <bool STATS, int SL, int WPB, int WW, int MINW, bool PERSIST = false, int MODE = 0>
 static hipError_t launch_one(const TraceParams& P, hipStream_t stream)
 {
@@ -554,7 +553,7 @@ static hipError_t launch_one(const TraceParams& P, hipStream_t stream)
         if (P.prioDealt) {
             // Every position dealt at the start runs in the first priority band.  Waves of equal
             // priority issue oldest first (the resident grid's dispatch order: tools/tile_trace.py shows
-            // the dealing rounds' tiles at 160 / 175 / 235 / 275 ms median and the last round's, at level
+            // the dealing rounds' tiles at 164 / 175 / 235 / 273 ms median and the last round's, at level
             // 2 below the others, at 373 ms -- the launch's end on the C4 N = 8 share); in one band the
             // order of the rounds follows the cost order.  C4 N = 8 share 464-481 -> 446-456 ms
             // (tools/prio_probe.py, profiles/r06_schedule_trace.json).
@@ -1476,7 +1475,7 @@ static int render_impl(pt_context* ctx, const pt_camera* cam, uint32_t spp, uint
                           (ctx->orderStale || !ctx->orderValid || (uint64_t)spp * chunks >= 4 * ctx->orderSamples);
     if (!rebuilds || ctx->prioMode == 2) issue_priority(ctx, units, P.prio);   // explicit bounds: always
     P.prioDealt = ctx->prioMode == 0 && P.prio[0] != 0;
-    if (ctx->traceTiles && P.tileCost) {
+    if (ctx->traceTiles && stats && P.tileCost) {
         if (ctx->tileTrace && ctx->traceCap < tiles) {
             (void)hipFree(ctx->tileTrace);
             ctx->tileTrace = nullptr;
